@@ -1,0 +1,955 @@
+// engine.hip -- MI355X (gfx950) kernels, per-device runtime and the C ABI of include/clay.h.
+//
+// Two device paths:
+//   * fused encode (k_fused_encode): the north-star path.  One workgroup owns a
+//     tile of W byte positions across ALL alpha layers of a stripe; it streams the
+//     data y-section by y-section (PRT on q x q (node, digit) blocks, then the
+//     per-layer RS parity contraction accumulated in LDS) and finishes with the
+//     PFT of the parity y-section.  Data bytes are read from HBM once, parity
+//     bytes written once, shortened (zero) nodes never touched.  Valid when the
+//     parity nodes form exactly the last y-section (q == m, i.e. d = k+m-1).
+//   * staged engine (k_exec): executes a Plan (plan.hpp) -- the reference's
+//     decode_layered / repair replayed into GF region ops -- one launch per
+//     dependency level, U-plane in an HBM workspace.  Used for decode, repair and
+//     encode shapes the fused kernel does not cover.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/clay.h"
+#include "code.hpp"
+#include "gf256.hpp"
+#include "kernels.hpp"
+#include "plan.hpp"
+
+namespace clay {
+
+constexpr int kMaxTn = 64;                 // internal nodes supported on device
+constexpr int kMaxBases = 2 * kMaxTn + 2;  // C[tn], H[tn], U, OUT
+constexpr int kExecBlock = 256;
+constexpr int kFusedBlock = 512;
+constexpr size_t kFusedLdsBudget = 128 * 1024;
+
+struct ExecPtrs {
+    uint8_t *p[kMaxBases];
+};
+
+// ---------------------------------------------------------------------------
+// Generic staged executor: one workgroup = one op x one tile of positions.
+// dst[pos] = XOR_s coef_s * src_s[pos]  over the op's sources.
+// ---------------------------------------------------------------------------
+template <int VW>
+__global__ __launch_bounds__(kExecBlock) void k_exec(ExecPtrs P, const DevOp *__restrict__ ops,
+                                                     const DevSrc *__restrict__ srcs,
+                                                     const uint32_t *__restrict__ tabs, uint32_t op0,
+                                                     uint32_t tiles, uint64_t sc) {
+    constexpr int NW = (VW + 3) / 4;
+    const uint32_t opi = blockIdx.x / tiles, tile = blockIdx.x - opi * tiles;
+    const DevOp op = ops[op0 + opi];
+    const uint64_t pos = (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
+    if (pos >= sc) return;
+    Words<NW> acc;
+#pragma unroll
+    for (int w = 0; w < NW; w++) acc.w[w] = 0;
+    for (uint32_t s = 0; s < op.nsrc; ++s) {
+        const DevSrc d = srcs[op.src_begin + s];
+        const Words<NW> v = vload<VW>(P.p[d.base] + uint64_t(d.slot) * sc + pos);
+        if (d.coef == 1) {
+#pragma unroll
+            for (int w = 0; w < NW; w++) acc.w[w] ^= v.w[w];
+        } else {
+            const GfTab t = load_tab(tabs + d.coef * 8);
+#pragma unroll
+            for (int w = 0; w < NW; w++) acc.w[w] ^= gf_mul(v.w[w], t);
+        }
+    }
+    vstore<VW>(P.p[op.base] + uint64_t(op.slot) * sc + pos, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Fused encode (parity = last y-section).  See file header and DESIGN.md.
+// LDS: acc[p][z][W] bytes (p < Q parity rows, z < alpha layers, W positions).
+// ---------------------------------------------------------------------------
+constexpr int kFusedMaxK = 64;
+struct FusedArgs {
+    const uint8_t *data[kFusedMaxK];  // internal nodes 0..K-1, nullptr = shortened (zero)
+    uint8_t *par[8];                  // parity y-section, node x
+    uint64_t sc;                      // sub-chunk size (bytes)
+    uint32_t alpha, t, K, W;          // layers, y-sections, K = k+nu, tile positions
+    uint32_t ntiles, tiles_per_xcd, nslots;
+    uint32_t dinv[5];                 // perm table of det^-1 (PFT, transforms.rs:307-308)
+};
+
+template <int Q, int PPT>
+__global__ __launch_bounds__(kFusedBlock) void k_fused_encode(FusedArgs a, const uint32_t *__restrict__ mtab) {
+    constexpr int NW = PPT / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t W = a.W, PG = W / PPT, alpha = a.alpha;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    GfTab dinv;
+    dinv.w0 = a.dinv[0]; dinv.w1 = a.dinv[1]; dinv.w2 = a.dinv[2]; dinv.w3 = a.dinv[3]; dinv.w4 = a.dinv[4];
+
+    for (uint32_t tix = slot; tix < a.tiles_per_xcd; tix += a.nslots) {
+        const uint32_t tile = xcd * a.tiles_per_xcd + tix;
+        if (tile >= a.ntiles) break;  // uniform per workgroup
+        const uint64_t b0 = uint64_t(tile) * W;
+
+        // ---- phase A: y-sections 0..t-2 -> parity-U accumulators in LDS ----
+        uint32_t wy = alpha / Q;  // q^(t-1-y), starting at y = 0
+        for (uint32_t y = 0; y + 1 < a.t; ++y, wy /= Q) {
+            const uint32_t nlines = alpha / Q, units = nlines * PG;
+            for (uint32_t u = threadIdx.x; u < units; u += kFusedBlock) {
+                const uint32_t line = u / PG, pg = u - line * PG;
+                const uint64_t pos = b0 + uint64_t(pg) * PPT;
+                const bool ok = pos < a.sc;
+                const uint32_t hi = line / wy, lo = line - hi * wy;
+                const uint32_t z0 = hi * wy * Q + lo;
+                uint32_t B[Q][Q][NW];
+#pragma unroll
+                for (int x = 0; x < Q; x++) {
+                    const uint8_t *nd = a.data[y * Q + x];
+#pragma unroll
+                    for (int j = 0; j < Q; j++) {
+                        if (nd != nullptr && ok) {
+                            Words<NW> v = vload<PPT>(nd + uint64_t(z0 + j * wy) * a.sc + pos);
+#pragma unroll
+                            for (int w = 0; w < NW; w++) B[x][j][w] = v.w[w];
+                        } else {
+#pragma unroll
+                            for (int w = 0; w < NW; w++) B[x][j][w] = 0;
+                        }
+                    }
+                }
+                // PRT on every off-diagonal pair: U[x][j] = C[x][j] + g*C[j][x]  (transforms.rs:42-55)
+#pragma unroll
+                for (int x = 0; x < Q; x++)
+#pragma unroll
+                    for (int j = x + 1; j < Q; j++)
+#pragma unroll
+                        for (int w = 0; w < NW; w++) {
+                            const uint32_t bxj = B[x][j][w], bjx = B[j][x][w];
+                            B[x][j][w] = bxj ^ gf_xt(bjx);
+                            B[j][x][w] = bjx ^ gf_xt(bxj);
+                        }
+                // RS parity rows: V[p][z_j] += M[p][yQ+x] * U[x][j]  (decode.rs:386-404)
+#pragma unroll
+                for (int j = 0; j < Q; j++) {
+                    uint32_t V[Q][NW];
+#pragma unroll
+                    for (int p = 0; p < Q; p++)
+#pragma unroll
+                        for (int w = 0; w < NW; w++) V[p][w] = 0;
+#pragma unroll
+                    for (int x = 0; x < Q; x++) {
+#pragma unroll
+                        for (int w = 0; w < NW; w++) {
+                            const GfIdx ix = gf_idx(B[x][j][w]);
+#pragma unroll
+                            for (int p = 0; p < Q; p++) {
+                                const GfTab tb = load_tab(mtab + (uint32_t(p) * a.K + y * Q + x) * 8);
+                                V[p][w] ^= gf_mul_idx(ix, tb);
+                            }
+                        }
+                    }
+                    const uint32_t z = z0 + j * wy;
+#pragma unroll
+                    for (int p = 0; p < Q; p++) {
+                        uint8_t *l = lds + (size_t(p) * alpha + z) * W + size_t(pg) * PPT;
+                        Words<NW> v;
+                        if (y == 0) {
+#pragma unroll
+                            for (int w = 0; w < NW; w++) v.w[w] = V[p][w];
+                        } else {
+                            v = vload<PPT>(l);
+#pragma unroll
+                            for (int w = 0; w < NW; w++) v.w[w] ^= V[p][w];
+                        }
+                        vstore<PPT>(l, v);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+
+        // ---- phase B: PFT of the parity y-section (digit t-1, weight 1) ----
+        {
+            const uint32_t ngroups = alpha / Q, units = ngroups * PG;
+            for (uint32_t u = threadIdx.x; u < units; u += kFusedBlock) {
+                const uint32_t g = u / PG, pg = u - g * PG;
+                const uint64_t pos = b0 + uint64_t(pg) * PPT;
+                const uint32_t z0 = g * Q;
+                uint32_t A[Q][Q][NW];
+#pragma unroll
+                for (int x = 0; x < Q; x++)
+#pragma unroll
+                    for (int j = 0; j < Q; j++) {
+                        Words<NW> v = vload<PPT>(lds + (size_t(x) * alpha + z0 + j) * W + size_t(pg) * PPT);
+#pragma unroll
+                        for (int w = 0; w < NW; w++) A[x][j][w] = v.w[w];
+                    }
+#pragma unroll
+                for (int x = 0; x < Q; x++)
+#pragma unroll
+                    for (int j = x + 1; j < Q; j++)
+#pragma unroll
+                        for (int w = 0; w < NW; w++) {  // C = det^-1 (U + g U*)  (transforms.rs:108-125)
+                            const uint32_t axj = A[x][j][w], ajx = A[j][x][w];
+                            A[x][j][w] = gf_mul(axj ^ gf_xt(ajx), dinv);
+                            A[j][x][w] = gf_mul(ajx ^ gf_xt(axj), dinv);
+                        }
+                if (pos < a.sc) {
+#pragma unroll
+                    for (int x = 0; x < Q; x++)
+#pragma unroll
+                        for (int j = 0; j < Q; j++) {
+                            Words<NW> v;
+#pragma unroll
+                            for (int w = 0; w < NW; w++) v.w[w] = A[x][j][w];
+                            vstore<PPT>(a.par[x] + uint64_t(z0 + j) * a.sc + pos, v);
+                        }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Runtime
+// ---------------------------------------------------------------------------
+#define CLAY_HIP(expr)                                                                                  \
+    do {                                                                                                \
+        hipError_t _e = (expr);                                                                         \
+        if (_e != hipSuccess)                                                                           \
+            return make_error(CLAY_ERR_DEVICE, size_t(_e), 0, 0, "HIP error: %s (%s)", hipGetErrorString(_e), \
+                              #expr);                                                                   \
+    } while (0)
+
+static std::mutex g_mu;
+static thread_local std::string t_last_path = "none";
+static thread_local size_t t_last_launches = 0;
+static int g_encode_mode = 0;
+
+struct Workspace {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct DevState {
+    bool init = false;
+    uint32_t *d_tabs = nullptr;                    // perm tables of all 256 constants
+    std::map<void *, Workspace> ws;                // per-stream U workspace
+    std::mutex host_mu;                            // serialises the host-buffer API per device
+    hipStream_t host_stream = nullptr;
+    Workspace host_bufs[3];
+};
+static DevState g_dev[64];
+
+struct CodeState {
+    clay_code_t code{};
+    RsCtx rs;
+    std::unique_ptr<Plan> enc;
+    std::map<std::vector<uint8_t>, std::unique_ptr<Plan>> dec, rep;
+    std::map<std::pair<const Plan *, int>, std::pair<void *, void *>> dplan;
+    std::map<int, uint32_t *> mtab;
+    explicit CodeState(const clay_code_t &c) : code(c), rs(c) {}
+};
+static std::map<std::tuple<size_t, size_t, size_t>, std::unique_ptr<CodeState>> g_codes;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+static Error check_code(const clay_code_t *c) {
+    if (!c) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null code");
+    clay_code_t chk{};
+    Error e = code_new(c->k, c->m, c->d, &chk);
+    if (e) return e;
+    if (std::memcmp(&chk, c, sizeof(chk)) != 0)
+        return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: code struct not produced by clay_new");
+    return Error{};
+}
+
+static Error dev_state(int dev, DevState **out) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: no GPU device available (no CPU fallback)");
+    if (dev < 0 || dev >= ndev || dev >= 64)
+        return make_error(CLAY_ERR_DEVICE, size_t(dev), 0, 0, "HIP error: invalid device ordinal %d", dev);
+    DevState &s = g_dev[dev];
+    if (!s.init) {
+        DeviceGuard g(dev);
+        std::vector<uint32_t> tabs(256 * 8);
+        for (int c = 0; c < 256; c++) perm_table(uint8_t(c), &tabs[c * 8]);
+        CLAY_HIP(hipMalloc(&s.d_tabs, tabs.size() * 4));
+        CLAY_HIP(hipMemcpy(s.d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+        s.init = true;
+    }
+    *out = &s;
+    return Error{};
+}
+
+static CodeState *code_state(const clay_code_t &c) {
+    auto key = std::make_tuple(c.k, c.m, c.d);
+    auto it = g_codes.find(key);
+    if (it != g_codes.end()) return it->second.get();
+    auto cs = std::make_unique<CodeState>(c);
+    CodeState *p = cs.get();
+    g_codes[key] = std::move(cs);
+    return p;
+}
+
+static Error upload_plan(CodeState &cs, const Plan &pl, int dev, const DevOp **ops, const DevSrc **srcs) {
+    auto key = std::make_pair(&pl, dev);
+    auto it = cs.dplan.find(key);
+    if (it == cs.dplan.end()) {
+        void *o = nullptr, *s = nullptr;
+        CLAY_HIP(hipMalloc(&o, std::max<size_t>(1, pl.ops.size()) * sizeof(DevOp)));
+        CLAY_HIP(hipMalloc(&s, std::max<size_t>(1, pl.srcs.size()) * sizeof(DevSrc)));
+        if (!pl.ops.empty()) CLAY_HIP(hipMemcpy(o, pl.ops.data(), pl.ops.size() * sizeof(DevOp), hipMemcpyHostToDevice));
+        if (!pl.srcs.empty())
+            CLAY_HIP(hipMemcpy(s, pl.srcs.data(), pl.srcs.size() * sizeof(DevSrc), hipMemcpyHostToDevice));
+        it = cs.dplan.emplace(key, std::make_pair(o, s)).first;
+    }
+    *ops = static_cast<const DevOp *>(it->second.first);
+    *srcs = static_cast<const DevSrc *>(it->second.second);
+    return Error{};
+}
+
+static Error ensure_ws(DevState &ds, void *stream, size_t bytes, void **out) {
+    Workspace &w = ds.ws[stream];
+    if (w.bytes < bytes) {
+        if (w.ptr) {
+            CLAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+            CLAY_HIP(hipFree(w.ptr));
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        CLAY_HIP(hipMalloc(&w.ptr, bytes));
+        w.bytes = bytes;
+    }
+    *out = w.ptr;
+    return Error{};
+}
+
+static int align_of(uintptr_t p) {
+    for (int a = 16; a > 1; a >>= 1)
+        if ((p % a) == 0) return a;
+    return 1;
+}
+
+// Execute a plan: C/H/OUT pointer bindings given, U workspace bound here.
+static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
+                      ExecPtrs ptrs, size_t sc, size_t chunk_for_ws) {
+    const DevOp *d_ops;
+    const DevSrc *d_srcs;
+    Error e = upload_plan(cs, pl, dev, &d_ops, &d_srcs);
+    if (e) return e;
+    if (pl.uses_u) {
+        void *ws = nullptr;
+        e = ensure_ws(ds, stream, size_t(pl.tn) * chunk_for_ws, &ws);
+        if (e) return e;
+        ptrs.p[2 * pl.tn] = static_cast<uint8_t *>(ws);
+    }
+    int vw = 16;
+    while (vw > 1 && (sc % vw) != 0) vw >>= 1;
+    for (int i = 0; i < kMaxBases; i++)
+        if (ptrs.p[i]) vw = std::min(vw, align_of(reinterpret_cast<uintptr_t>(ptrs.p[i])));
+    const uint64_t per_thread = uint64_t(vw);
+    const uint32_t tiles = uint32_t((sc / per_thread + kExecBlock - 1) / kExecBlock);
+    size_t launches = 0;
+    for (size_t s = 0; s + 1 < pl.stage_begin.size(); s++) {
+        uint32_t b = pl.stage_begin[s], end = pl.stage_begin[s + 1];
+        while (b < end) {
+            uint32_t nops = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
+            dim3 grid(nops * tiles), block(kExecBlock);
+            switch (vw) {
+            case 16: k_exec<16><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
+            case 8: k_exec<8><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
+            case 4: k_exec<4><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
+            case 2: k_exec<2><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
+            default: k_exec<1><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
+            }
+            CLAY_HIP(hipGetLastError());
+            launches++;
+            b += nops;
+        }
+    }
+    t_last_launches += launches;
+    return Error{};
+}
+
+// ---------------------------------------------------------------------------
+// Encode paths
+// ---------------------------------------------------------------------------
+static bool fused_shape_ok(const clay_code_t &c) {
+    return c.q == c.m && c.k + c.nu == (c.t - 1) * c.q && c.q >= 2 && c.q <= 4 && c.original_count <= kFusedMaxK;
+}
+
+template <int Q, int PPT>
+static Error launch_fused(const FusedArgs &a, const uint32_t *mtab, size_t lds, hipStream_t stream, int grid) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fused_encode<Q, PPT>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(kFusedLdsBudget)));
+        attr_set = true;
+    }
+    k_fused_encode<Q, PPT><<<dim3(grid), dim3(kFusedBlock), lds, stream>>>(a, mtab);
+    CLAY_HIP(hipGetLastError());
+    return Error{};
+}
+
+static Error encode_fused(CodeState &cs, DevState &ds, int dev, const uint8_t *const *data, uint8_t *const *par,
+                          size_t n_stripes, size_t chunk, hipStream_t stream, bool *done) {
+    *done = false;
+    const clay_code_t &c = cs.code;
+    if (!fused_shape_ok(c)) return Error{};
+    const size_t alpha = c.sub_chunk_no, sc = chunk / alpha, K = c.original_count, Q = c.q;
+    int ppt = 16;
+    while (ppt >= 4 && (sc % ppt) != 0) ppt >>= 1;
+    if (ppt < 4) return Error{};
+    for (size_t s = 0; s < n_stripes; s++) {
+        for (size_t i = 0; i < c.k; i++) ppt = std::min(ppt, align_of(reinterpret_cast<uintptr_t>(data[s * c.k + i])));
+        for (size_t i = 0; i < c.m; i++) ppt = std::min(ppt, align_of(reinterpret_cast<uintptr_t>(par[s * c.m + i])));
+    }
+    if (ppt < 4) return Error{};
+    size_t W = (kFusedLdsBudget / (Q * alpha)) / size_t(ppt) * size_t(ppt);
+    W = std::min<size_t>(W, 2048);
+    if (W < size_t(ppt)) return Error{};
+    // device RS parity rows as perm tables [p][i][8]
+    auto it = cs.mtab.find(dev);
+    if (it == cs.mtab.end()) {
+        std::vector<uint32_t> t(Q * K * 8);
+        for (size_t p = 0; p < Q; p++)
+            for (size_t i = 0; i < K; i++) perm_table(cs.rs.gen[(K + p) * K + i], &t[(p * K + i) * 8]);
+        uint32_t *d = nullptr;
+        CLAY_HIP(hipMalloc(&d, t.size() * 4));
+        CLAY_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        it = cs.mtab.emplace(dev, d).first;
+    }
+    hipDeviceProp_t prop;
+    CLAY_HIP(hipGetDeviceProperties(&prop, dev));
+    const size_t lds = Q * alpha * W;
+    const int per_cu = std::max<int>(1, int((160 * 1024) / lds));
+    for (size_t s = 0; s < n_stripes; s++) {
+        FusedArgs a{};
+        for (size_t i = 0; i < K; i++) a.data[i] = i < c.k ? data[s * c.k + i] : nullptr;
+        for (size_t x = 0; x < Q; x++) a.par[x] = par[s * c.m + x];
+        a.sc = sc;
+        a.alpha = uint32_t(alpha);
+        a.t = uint32_t(c.t);
+        a.K = uint32_t(K);
+        a.W = uint32_t(W);
+        a.ntiles = uint32_t((sc + W - 1) / W);
+        a.tiles_per_xcd = (a.ntiles + 7) / 8;
+        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
+        a.nslots = std::min(max_slots, a.tiles_per_xcd);
+        uint32_t w[8];
+        perm_table(gamma_det_inv(), w);
+        for (int i = 0; i < 5; i++) a.dinv[i] = w[i];
+        const int grid = int(a.nslots * 8);
+        Error e;
+        switch (Q * 100 + ppt) {
+        case 216: e = launch_fused<2, 16>(a, it->second, lds, stream, grid); break;
+        case 208: e = launch_fused<2, 8>(a, it->second, lds, stream, grid); break;
+        case 204: e = launch_fused<2, 4>(a, it->second, lds, stream, grid); break;
+        case 316: e = launch_fused<3, 16>(a, it->second, lds, stream, grid); break;
+        case 308: e = launch_fused<3, 8>(a, it->second, lds, stream, grid); break;
+        case 304: e = launch_fused<3, 4>(a, it->second, lds, stream, grid); break;
+        case 416: e = launch_fused<4, 16>(a, it->second, lds, stream, grid); break;
+        case 408: e = launch_fused<4, 8>(a, it->second, lds, stream, grid); break;
+        case 404: e = launch_fused<4, 4>(a, it->second, lds, stream, grid); break;
+        default: return Error{};
+        }
+        if (e) return e;
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "fused-q%zuw%zup%d", Q, W, ppt);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
+static Error encode_staged(CodeState &cs, DevState &ds, int dev, const uint8_t *const *data, uint8_t *const *par,
+                           size_t n_stripes, size_t chunk, hipStream_t stream) {
+    const clay_code_t &c = cs.code;
+    if (c.q * c.t > size_t(kMaxTn))
+        return make_error(CLAY_ERR_DEVICE, c.q * c.t, 0, 0, "device engine supports at most %d internal nodes", kMaxTn);
+    if (!cs.enc) {
+        Error e = plan_encode(c, cs.rs, cs.enc);
+        if (e) return e;
+    }
+    const size_t sc = chunk / c.sub_chunk_no;
+    for (size_t s = 0; s < n_stripes; s++) {
+        ExecPtrs P{};
+        for (size_t i = 0; i < c.k; i++) P.p[i] = const_cast<uint8_t *>(data[s * c.k + i]);
+        for (size_t i = 0; i < c.m; i++) P.p[c.k + c.nu + i] = par[s * c.m + i];
+        Error e = run_plan(cs, *cs.enc, dev, ds, stream, P, sc, chunk);
+        if (e) return e;
+    }
+    t_last_path = "staged";
+    return Error{};
+}
+
+static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *data, uint8_t *const *par,
+                                size_t n_stripes, size_t chunk, int dev, void *stream) {
+    Error e = check_code(code);
+    if (e) return e;
+    if (!data || !par) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null chunk array");
+    if (chunk == 0 || chunk % code->sub_chunk_no != 0)
+        return make_error(CLAY_ERR_INVALID_CHUNK_SIZE, code->sub_chunk_no, chunk, 0,
+                          "Invalid chunk size: expected divisible by %zu, got %zu", code->sub_chunk_no, chunk);
+    for (size_t i = 0; i < n_stripes * code->k; i++)
+        if (!data[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null data chunk");
+    for (size_t i = 0; i < n_stripes * code->m; i++)
+        if (!par[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk");
+    std::lock_guard<std::mutex> lk(g_mu);
+    t_last_launches = 0;
+    DevState *ds;
+    e = dev_state(dev, &ds);
+    if (e) return e;
+    DeviceGuard g(dev);
+    CodeState &cs = *code_state(*code);
+    if (cs.rs.init_err)
+        return make_error(CLAY_ERR_RECONSTRUCTION_FAILED, 0, 0, 0, "RS reconstruction failed: RS init failed: %s",
+                          rs_error_name(cs.rs.init_err));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (g_encode_mode != 1) {
+        bool done = false;
+        e = encode_fused(cs, *ds, dev, data, par, n_stripes, chunk, st, &done);
+        if (e || done) return e;
+        if (g_encode_mode == 2)
+            return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "fused encode kernel does not support this code/alignment");
+    }
+    return encode_staged(cs, *ds, dev, data, par, n_stripes, chunk, st);
+}
+
+// ---------------------------------------------------------------------------
+// Decode / repair on device
+// ---------------------------------------------------------------------------
+static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
+                                uint8_t *const *outs, size_t chunk, int dev, void *stream) {
+    Error e = check_code(code);
+    if (e) return e;
+    const clay_code_t &c = *code;
+    if (!chunks || !outs) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null chunk array");
+    std::vector<size_t> ids, lens;
+    for (size_t i = 0; i < c.n; i++)
+        if (chunks[i]) {
+            ids.push_back(i);
+            lens.push_back(chunk);
+        }
+    if (ids.empty() && ner == 0) return Error{};
+    size_t cs_sz = 0;
+    std::vector<uint8_t> erased;
+    e = validate_decode(c, AvailView{ids.data(), lens.data(), ids.size()}, er, ner, &cs_sz, erased);
+    if (e) return e;
+    const size_t tn = c.q * c.t;
+    std::vector<uint8_t> want(tn, 0);
+    for (size_t i = 0; i < ner; i++) {
+        size_t in = internal_of(c, er[i]);
+        if (er[i] < c.k && !outs[er[i]])
+            return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: no output buffer for erased node %zu",
+                              er[i]);
+        want[in] = outs[er[i]] ? 1 : 0;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    t_last_launches = 0;
+    DevState *ds;
+    e = dev_state(dev, &ds);
+    if (e) return e;
+    DeviceGuard g(dev);
+    CodeState &cs = *code_state(c);
+    if (tn > size_t(kMaxTn))
+        return make_error(CLAY_ERR_DEVICE, tn, 0, 0, "device engine supports at most %d internal nodes", kMaxTn);
+    std::vector<uint8_t> key(erased);
+    key.insert(key.end(), want.begin(), want.end());
+    auto it = cs.dec.find(key);
+    if (it == cs.dec.end()) {
+        std::unique_ptr<Plan> p;
+        e = plan_decode(c, cs.rs, erased, want, p);
+        if (e) return e;
+        it = cs.dec.emplace(key, std::move(p)).first;
+    }
+    ExecPtrs P{};
+    for (size_t i = 0; i < c.n; i++) {
+        size_t in = internal_of(c, i);
+        P.p[in] = chunks[i] ? const_cast<uint8_t *>(chunks[i]) : (want[in] ? outs[i] : nullptr);
+    }
+    return run_plan(cs, *it->second, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
+}
+
+static Error repair_device_impl(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs,
+                                const size_t *lens, size_t nh, size_t chunk, uint8_t *out, int dev, void *stream) {
+    Error e = check_code(code);
+    if (e) return e;
+    const clay_code_t &c = *code;
+    std::vector<uint8_t> hin;
+    std::vector<long> slot_of;
+    std::vector<size_t> sub;
+    e = validate_repair(c, lost, ids, lens, nh, chunk, hin, slot_of, sub);
+    if (e) return e;
+    if (!out) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output");
+    std::lock_guard<std::mutex> lk(g_mu);
+    t_last_launches = 0;
+    DevState *ds;
+    e = dev_state(dev, &ds);
+    if (e) return e;
+    DeviceGuard g(dev);
+    const size_t tn = c.q * c.t;
+    if (tn > size_t(kMaxTn))
+        return make_error(CLAY_ERR_DEVICE, tn, 0, 0, "device engine supports at most %d internal nodes", kMaxTn);
+    CodeState &cs = *code_state(c);
+    std::vector<uint8_t> key(hin);
+    key.push_back(uint8_t(lost & 0xFF));
+    key.push_back(uint8_t(lost >> 8));
+    auto it = cs.rep.find(key);
+    if (it == cs.rep.end()) {
+        std::unique_ptr<Plan> p;
+        e = plan_repair(c, cs.rs, lost, hin, slot_of, sub, p);
+        if (e) return e;
+        it = cs.rep.emplace(key, std::move(p)).first;
+    }
+    ExecPtrs P{};
+    for (size_t in = 0; in < tn; in++)
+        if (slot_of[in] >= 0) P.p[tn + in] = const_cast<uint8_t *>(bufs[slot_of[in]]);
+    P.p[2 * tn + 1] = out;
+    return run_plan(cs, *it->second, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
+}
+
+// ---------------------------------------------------------------------------
+// Host-buffer API helpers: device staging buffers per device.
+// ---------------------------------------------------------------------------
+static Error host_buf(DevState &ds, int which, size_t bytes, uint8_t **out) {
+    Workspace &w = ds.host_bufs[which];
+    if (w.bytes < bytes) {
+        if (w.ptr) CLAY_HIP(hipFree(w.ptr));
+        w.ptr = nullptr;
+        w.bytes = 0;
+        CLAY_HIP(hipMalloc(&w.ptr, std::max<size_t>(bytes, 1)));
+        w.bytes = bytes;
+    }
+    *out = static_cast<uint8_t *>(w.ptr);
+    return Error{};
+}
+
+static Error host_device(int *dev, DevState **ds) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: no GPU device available (no CPU fallback)");
+    int d = 0;
+    (void)hipGetDevice(&d);
+    *dev = d;
+    Error e;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        e = dev_state(d, ds);
+    }
+    if (e) return e;
+    if (!(*ds)->host_stream) CLAY_HIP(hipStreamCreateWithFlags(&(*ds)->host_stream, hipStreamNonBlocking));
+    return Error{};
+}
+
+}  // namespace clay
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace clay;
+
+extern "C" {
+
+int clay_abi_version(void) { return CLAY_ABI_VERSION; }
+const char *clay_build_info(void) { return "clay_amd " __DATE__ " gfx950 HIP"; }
+int clay_set_encode_path(int mode) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int prev = g_encode_mode;
+    g_encode_mode = mode;
+    return prev;
+}
+const char *clay_last_encode_path(void) { return t_last_path.c_str(); }
+size_t clay_last_launch_count(void) { return t_last_launches; }
+
+int clay_new(size_t k, size_t m, size_t d, clay_code_t *out, clay_error_t *err) {
+    if (!out) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output"), err);
+    Error e = code_new(k, m, d, out);
+    if (err) std::memset(err, 0, sizeof(*err));
+    return e ? report(e, err) : 0;
+}
+int clay_new_default(size_t k, size_t m, clay_code_t *out, clay_error_t *err) {
+    return clay_new(k, m, k + m - 1, out, err);
+}
+double clay_normalized_repair_bandwidth(const clay_code_t *c) {
+    return double(c->d) / (double(c->k) * double(c->d - c->k + 1));
+}
+size_t clay_encoded_chunk_size(const clay_code_t *c, size_t len) { return encoded_chunk_size(*c, len); }
+
+int clay_minimum_to_repair(const clay_code_t *code, size_t lost, const size_t *avail, size_t nav, size_t *helpers_out,
+                           size_t *n_helpers, size_t *sub_out, size_t *n_sub, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    std::vector<size_t> h, s;
+    e = minimum_to_repair(*code, lost, avail, nav, h, s);
+    if (n_helpers) *n_helpers = h.size();
+    if (n_sub) *n_sub = e ? 0 : s.size();
+    if (e) return report(e, err);
+    if (helpers_out) std::copy(h.begin(), h.end(), helpers_out);
+    if (sub_out) std::copy(s.begin(), s.end(), sub_out);
+    return 0;
+}
+
+int clay_encode_device(const clay_code_t *code, const uint8_t *const *data, uint8_t *const *par, size_t chunk,
+                       int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = encode_device_impl(code, data, par, 1, chunk, device, stream);
+    return e ? report(e, err) : 0;
+}
+
+int clay_encode_device_batch(const clay_code_t *code, const uint8_t *const *data, uint8_t *const *par, size_t ns,
+                             size_t chunk, int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = encode_device_impl(code, data, par, ns, chunk, device, stream);
+    return e ? report(e, err) : 0;
+}
+
+int clay_decode_device(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
+                       uint8_t *const *outs, size_t chunk, int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = decode_device_impl(code, chunks, er, ner, outs, chunk, device, stream);
+    return e ? report(e, err) : 0;
+}
+
+int clay_repair_device(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs, size_t nh,
+                       size_t chunk, uint8_t *out, int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = repair_device_impl(code, lost, ids, bufs, nullptr, nh, chunk, out, device, stream);
+    return e ? report(e, err) : 0;
+}
+
+int clay_reserve_workspace(const clay_code_t *code, size_t chunk, int device, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevState *ds;
+    e = dev_state(device, &ds);
+    if (e) return report(e, err);
+    DeviceGuard g(device);
+    void *p;
+    e = ensure_ws(*ds, nullptr, code->q * code->t * chunk, &p);
+    return e ? report(e, err) : 0;
+}
+
+int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, const uint8_t *want, size_t lost,
+                     uint32_t *ops_out, size_t ops_cap, uint32_t *srcs_out, size_t srcs_cap, uint32_t *stages_out,
+                     size_t stages_cap, size_t counts[3], clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    const clay_code_t &c = *code;
+    const size_t tn = c.q * c.t;
+    RsCtx rs(c);
+    std::unique_ptr<Plan> p;
+    if (kind == 0) {
+        e = plan_encode(c, rs, p);
+    } else if (kind == 1) {
+        if (!mask || !want) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null mask"), err);
+        e = plan_decode(c, rs, std::vector<uint8_t>(mask, mask + tn), std::vector<uint8_t>(want, want + tn), p);
+    } else if (kind == 2) {
+        if (!mask) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null mask"), err);
+        std::vector<uint8_t> hin(mask, mask + tn);
+        std::vector<long> so(tn, -1);
+        std::vector<size_t> sub;
+        if (lost >= c.n)
+            return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: Invalid lost node index: %zu >= %zu", lost, c.n), err);
+        e = repair_subchunk_indices(c, internal_of(c, lost), sub);
+        if (!e) e = plan_repair(c, rs, lost, hin, so, sub, p);
+    } else {
+        e = make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: plan kind %d", kind);
+    }
+    if (e) return report(e, err);
+    if (counts) {
+        counts[0] = p->ops.size();
+        counts[1] = p->srcs.size();
+        counts[2] = p->stage_begin.size();
+    }
+    if (ops_out && ops_cap >= p->ops.size() * 4 && srcs_out && srcs_cap >= p->srcs.size() * 4 && stages_out &&
+        stages_cap >= p->stage_begin.size()) {
+        for (size_t i = 0; i < p->ops.size(); i++) {
+            ops_out[4 * i] = p->ops[i].base;
+            ops_out[4 * i + 1] = p->ops[i].slot;
+            ops_out[4 * i + 2] = p->ops[i].src_begin;
+            ops_out[4 * i + 3] = p->ops[i].nsrc;
+        }
+        for (size_t i = 0; i < p->srcs.size(); i++) {
+            srcs_out[4 * i] = p->srcs[i].base;
+            srcs_out[4 * i + 1] = p->srcs[i].slot;
+            srcs_out[4 * i + 2] = p->srcs[i].coef;
+            srcs_out[4 * i + 3] = 0;
+        }
+        std::copy(p->stage_begin.begin(), p->stage_begin.end(), stages_out);
+    }
+    return 0;
+}
+
+int clay_encode(const clay_code_t *code, const uint8_t *data, size_t len, uint8_t *const *out, size_t chunk,
+                clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    const clay_code_t &c = *code;
+    if (!out) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output"), err);
+    size_t expect = encoded_chunk_size(c, len);
+    if (chunk != expect)
+        return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0,
+                                 "Invalid parameters: chunk_size %zu does not match encoded chunk size %zu", chunk,
+                                 expect),
+                      err);
+    for (size_t i = 0; i < c.n; i++)
+        if (!out[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output chunk"), err);
+    // data chunks: zero-padded copy of the input (encode.rs:44-55)
+    for (size_t i = 0; i < c.k; i++) {
+        size_t lo = i * chunk, n = lo < len ? std::min(chunk, len - lo) : 0;
+        if (n) std::memcpy(out[i], data + lo, n);
+        if (n < chunk) std::memset(out[i] + n, 0, chunk - n);
+    }
+    int dev;
+    DevState *ds;
+    e = host_device(&dev, &ds);
+    if (e) return report(e, err);
+    std::lock_guard<std::mutex> hl(ds->host_mu);
+    uint8_t *d_data, *d_par;
+    if ((e = host_buf(*ds, 0, c.k * chunk, &d_data)) || (e = host_buf(*ds, 1, c.m * chunk, &d_par))) return report(e, err);
+    hipStream_t st = ds->host_stream;
+    auto fail = [&](hipError_t he) {
+        return report(make_error(CLAY_ERR_DEVICE, size_t(he), 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+    };
+    hipError_t he;
+    if (len && (he = hipMemcpyAsync(d_data, data, len, hipMemcpyHostToDevice, st)) != hipSuccess) return fail(he);
+    if (c.k * chunk > len && (he = hipMemsetAsync(d_data + len, 0, c.k * chunk - len, st)) != hipSuccess) return fail(he);
+    std::vector<const uint8_t *> dp(c.k);
+    std::vector<uint8_t *> pp(c.m);
+    for (size_t i = 0; i < c.k; i++) dp[i] = d_data + i * chunk;
+    for (size_t i = 0; i < c.m; i++) pp[i] = d_par + i * chunk;
+    e = encode_device_impl(code, dp.data(), pp.data(), 1, chunk, dev, st);
+    if (e) return report(e, err);
+    for (size_t i = 0; i < c.m; i++)
+        if ((he = hipMemcpyAsync(out[c.k + i], pp[i], chunk, hipMemcpyDeviceToHost, st)) != hipSuccess) return fail(he);
+    if ((he = hipStreamSynchronize(st)) != hipSuccess) return fail(he);
+    return 0;
+}
+
+int clay_decode(const clay_code_t *code, const size_t *ids, const uint8_t *const *bufs, const size_t *lens,
+                size_t n_avail, const size_t *er, size_t ner, uint8_t *out, size_t out_cap, size_t *out_len,
+                clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    if (out_len) *out_len = 0;
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    const clay_code_t &c = *code;
+    if (n_avail == 0 && ner == 0) return 0;
+    size_t chunk = 0;
+    std::vector<uint8_t> erased;
+    e = validate_decode(c, AvailView{ids, lens, n_avail}, er, ner, &chunk, erased);
+    if (e) return report(e, err);
+    const size_t need = c.k * chunk;
+    if (!out || out_cap < need)
+        return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: output buffer too small"), err);
+    std::vector<const uint8_t *> host_of(c.n, nullptr);
+    for (size_t i = 0; i < n_avail; i++) host_of[ids[i]] = bufs[i];
+    for (size_t i = 0; i < c.k; i++)
+        if (host_of[i]) std::memcpy(out + i * chunk, host_of[i], chunk);
+    bool any_data_erased = false;
+    for (size_t i = 0; i < ner; i++) any_data_erased |= er[i] < c.k;
+    if (any_data_erased) {
+        int dev;
+        DevState *ds;
+        e = host_device(&dev, &ds);
+        if (e) return report(e, err);
+        std::lock_guard<std::mutex> hl(ds->host_mu);
+        uint8_t *d_in, *d_out;
+        if ((e = host_buf(*ds, 0, n_avail * chunk, &d_in)) || (e = host_buf(*ds, 1, c.k * chunk, &d_out)))
+            return report(e, err);
+        hipStream_t st = ds->host_stream;
+        std::vector<const uint8_t *> dch(c.n, nullptr);
+        std::vector<uint8_t *> douts(c.n, nullptr);
+        hipError_t he;
+        for (size_t i = 0; i < n_avail; i++) {
+            he = hipMemcpyAsync(d_in + i * chunk, bufs[i], chunk, hipMemcpyHostToDevice, st);
+            if (he != hipSuccess) return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+            dch[ids[i]] = d_in + i * chunk;
+        }
+        for (size_t i = 0; i < ner; i++)
+            if (er[i] < c.k) douts[er[i]] = d_out + er[i] * chunk;
+        e = decode_device_impl(code, dch.data(), er, ner, douts.data(), chunk, dev, st);
+        if (e) return report(e, err);
+        for (size_t i = 0; i < ner; i++)
+            if (er[i] < c.k) {
+                he = hipMemcpyAsync(out + er[i] * chunk, douts[er[i]], chunk, hipMemcpyDeviceToHost, st);
+                if (he != hipSuccess) return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+            }
+        he = hipStreamSynchronize(st);
+        if (he != hipSuccess) return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+    }
+    if (out_len) *out_len = need;
+    return 0;
+}
+
+int clay_repair(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs, const size_t *lens,
+                size_t nh, size_t chunk, uint8_t *out, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    const clay_code_t &c = *code;
+    {
+        std::vector<uint8_t> hin;
+        std::vector<long> so;
+        std::vector<size_t> sub;
+        e = validate_repair(c, lost, ids, lens, nh, chunk, hin, so, sub);
+        if (e) return report(e, err);
+    }
+    if (!out) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output"), err);
+    int dev;
+    DevState *ds;
+    e = host_device(&dev, &ds);
+    if (e) return report(e, err);
+    std::lock_guard<std::mutex> hl(ds->host_mu);
+    const size_t hb = lens[0];
+    uint8_t *d_in, *d_out;
+    if ((e = host_buf(*ds, 0, nh * hb, &d_in)) || (e = host_buf(*ds, 1, chunk, &d_out))) return report(e, err);
+    hipStream_t st = ds->host_stream;
+    std::vector<const uint8_t *> dh(nh);
+    hipError_t he;
+    for (size_t i = 0; i < nh; i++) {
+        dh[i] = d_in + i * hb;
+        if (hb && (he = hipMemcpyAsync(d_in + i * hb, bufs[i], hb, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+    }
+    e = repair_device_impl(code, lost, ids, dh.data(), lens, nh, chunk, d_out, dev, st);
+    if (e) return report(e, err);
+    if ((he = hipMemcpyAsync(out, d_out, chunk, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (he = hipStreamSynchronize(st)) != hipSuccess)
+        return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+// plan.hpp -- symbolic replay of the reference's layered algorithms into a
+// staged list of GF(2^8) region operations executed by the GPU.
+//
+// Every byte operation of the reference (PRT/PFT and partial transforms,
+// transforms.rs:42-161; red copies, decode.rs:284-289/245-250; per-layer RS
+// encode/reconstruct, decode.rs:332-408; repair phases, repair.rs:309-416) is a
+// GF-linear combination of whole sub-chunks:   dst = XOR_j coef_j * src_j.
+// The planner runs the reference control flow (iscore order, u_computed
+// tracking, per-layer erasure sets, RS row selection) on region NAMES instead
+// of bytes, so the emitted op DAG computes exactly the reference's linear map --
+// byte-identical output for any input, codeword or not.  It then removes dead
+// ops and groups the rest into dependency levels (one kernel launch per level).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <unordered_map>
+#include <vector>
+
+#include "code.hpp"
+
+namespace clay {
+
+enum RegionKind : uint32_t { RK_C = 0, RK_H = 1, RK_U = 2, RK_OUT = 3 };
+
+inline uint64_t rkey(uint32_t kind, uint32_t node, uint32_t slot) {
+    return (uint64_t(kind) << 56) | (uint64_t(node) << 32) | uint64_t(slot);
+}
+inline uint32_t rkind(uint64_t k) { return uint32_t(k >> 56); }
+inline uint32_t rnode(uint64_t k) { return uint32_t((k >> 32) & 0xFFFFFF); }
+inline uint32_t rslot(uint64_t k) { return uint32_t(k); }
+
+// Device-side records (kernel reads these).
+struct DevSrc {
+    uint32_t base;  // pointer-table index
+    uint32_t slot;  // sub-chunk index within that buffer
+    uint32_t coef;  // GF(2^8) coefficient (1..255)
+    uint32_t pad;
+};
+struct DevOp {
+    uint32_t base, slot;       // destination
+    uint32_t src_begin, nsrc;  // into DevSrc array
+};
+
+struct Plan {
+    // pointer table layout: [0, tn) = C[node], [tn, 2tn) = H[node], 2tn = U workspace
+    // (slot = node*alpha + z), 2tn+1 = OUT.
+    uint32_t tn = 0, alpha = 0;
+    std::vector<DevOp> ops;           // grouped by stage
+    std::vector<DevSrc> srcs;
+    std::vector<uint32_t> stage_begin;  // size = stages + 1
+    bool uses_u = false;
+    size_t total_src_terms = 0;
+    // device copies (owned by the runtime, per device)
+    void *d_ops = nullptr, *d_srcs = nullptr;
+    int device = -1;
+};
+
+class PlanBuilder {
+  public:
+    struct Term {
+        uint64_t key;
+        int32_t ver;  // producing op index, -1 = external input
+        uint8_t coef;
+    };
+    struct Op {
+        uint64_t dst;
+        int32_t prev;  // previous version of dst (-1 none)
+        std::vector<Term> src;
+    };
+
+    std::vector<Op> ops;
+    std::unordered_map<uint64_t, int32_t> cur;  // region -> current version
+    std::vector<uint8_t> zero_c, zero_h;          // per internal node: C / H input is known zero
+
+    // dst = XOR coef*src; terms on zero regions / zero coefs are dropped.
+    void emit(uint64_t dst, const std::vector<std::pair<uint64_t, uint8_t>> &terms);
+    std::unique_ptr<Plan> finalize(const std::vector<uint64_t> &outputs, uint32_t tn, uint32_t alpha);
+
+  private:
+    bool is_zero(uint64_t key, int32_t ver) const;
+};
+
+// Per-code RS cache (generator rows + reconstruct matrices by valid-row set).
+struct RsCtx {
+    size_t K = 0, M = 0, T = 0;
+    std::vector<uint8_t> gen;  // T x K
+    int init_err = 0;
+    std::unordered_map<std::string, std::vector<uint8_t>> inv_cache;
+    explicit RsCtx(const clay_code_t &c);
+    const std::vector<uint8_t> *inverse_for(const std::vector<size_t> &valid);
+};
+
+// encode = decode_layered with the parity nodes erased (encode.rs:57-68).
+Error plan_encode(const clay_code_t &c, RsCtx &rs, std::unique_ptr<Plan> &out);
+// decode.rs:152 decode_layered over the erased set; outputs = C of the erased
+// internal nodes whose want_out flag is set.
+Error plan_decode(const clay_code_t &c, RsCtx &rs, const std::vector<uint8_t> &erased,
+                  const std::vector<uint8_t> &want_out, std::unique_ptr<Plan> &out);
+// repair.rs:140-421 with the given helper set (internal ids) and index list.
+Error plan_repair(const clay_code_t &c, RsCtx &rs, size_t lost, const std::vector<uint8_t> &helper_int,
+                  const std::vector<long> &slot_of_id, const std::vector<size_t> &subchunks,
+                  std::unique_ptr<Plan> &out);
+
+}  // namespace clay

@@ -1,0 +1,197 @@
+/*
+ * clay.h -- C ABI of the MI355X-native Clay (Coupled-Layer MSR) erasure-code engine.
+ *
+ * Drop-in boundary for the `ClayCode` API of spool-labs/clay (crate clay-codes
+ * 0.1.2).  Every entry point names the reference interface it replaces.  The
+ * signatures use plain pointers and sizes only (no torch / HIP types): a Rust
+ * `extern "C"` block, ctypes, JNI or cgo binds them directly.
+ *
+ * Conventions
+ *   - Return value: 0 on success, otherwise the error kind (enum clay_error_kind);
+ *     if `err` is non-NULL it receives kind, payload fields and the Display text
+ *     of the reference's ClayError (error.rs:26-54).
+ *   - All buffers are caller-allocated; size-query helpers replace Rust's owned
+ *     Vec returns.  `HashMap<usize, Vec<u8>>` arguments become parallel arrays
+ *     (ids[i], bufs[i], lens[i]); where the reference depends on HashMap
+ *     iteration order (decode.rs:54-56, repair.rs:225) this ABI uses array order.
+ *   - Thread safety: like the reference (ClayCode is immutable, lib.rs:58), all
+ *     functions may be called concurrently; internal per-device caches are locked.
+ *   - Host-buffer functions (clay_encode / clay_decode / clay_repair) copy to the
+ *     GPU, run the HIP kernels and copy back.  *_device functions take device
+ *     pointers and a hipStream_t (passed as void*) and are asynchronous.
+ *   - There is no CPU fallback: without a usable GPU, compute entry points fail
+ *     with CLAY_ERR_DEVICE.
+ */
+#ifndef CLAY_H
+#define CLAY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLAY_ABI_VERSION 1
+
+/* ClayCode public fields (lib.rs:59-82) + the two private RS counts (lib.rs:79-81). */
+typedef struct clay_code {
+    size_t k, m, n, d, q, t, nu, sub_chunk_no, beta;
+    size_t original_count, recovery_count;
+} clay_code_t;
+
+/* ClayError (error.rs:5-24).  Payload fields a,b,c follow declaration order:
+ *   InsufficientHelpers{needed, provided}           -> a, b
+ *   InvalidChunkSize{expected, actual}              -> a, b
+ *   InsufficientHelperData{helper, expected, actual}-> a, b, c
+ *   InconsistentChunkSizes{first_size, mismatched_idx, mismatched_size} -> a, b, c
+ *   TooManyErasures{max, actual}                    -> a, b
+ *   MissingYSectionHelper{lost_node, missing_helper}-> a, b
+ * String variants carry their text in msg only. */
+enum clay_error_kind {
+    CLAY_OK = 0,
+    CLAY_ERR_INVALID_PARAMETERS = 1,
+    CLAY_ERR_INSUFFICIENT_HELPERS = 2,
+    CLAY_ERR_INVALID_CHUNK_SIZE = 3,
+    CLAY_ERR_INSUFFICIENT_HELPER_DATA = 4,
+    CLAY_ERR_INCONSISTENT_CHUNK_SIZES = 5,
+    CLAY_ERR_TOO_MANY_ERASURES = 6,
+    CLAY_ERR_RECONSTRUCTION_FAILED = 7,
+    CLAY_ERR_MISSING_Y_SECTION_HELPER = 8,
+    CLAY_ERR_OVERFLOW = 9,
+    /* not in the reference: HIP runtime / device failure, unsupported device shape */
+    CLAY_ERR_DEVICE = 100,
+};
+
+typedef struct clay_error {
+    int kind;
+    size_t a, b, c;
+    char msg[256];
+} clay_error_t;
+
+/* ------------------------------------------------------------------ */
+/* Parameters                                                          */
+/* ------------------------------------------------------------------ */
+
+/* ClayCode::new(k, m, d)            -- lib.rs:94-147 */
+int clay_new(size_t k, size_t m, size_t d, clay_code_t *out, clay_error_t *err);
+/* ClayCode::new_default(k, m)       -- lib.rs:150-152 (d = k + m - 1) */
+int clay_new_default(size_t k, size_t m, clay_code_t *out, clay_error_t *err);
+/* ClayCode::normalized_repair_bandwidth -- lib.rs:239-241 */
+double clay_normalized_repair_bandwidth(const clay_code_t *code);
+/* Chunk size ClayCode::encode produces for `data_len` bytes -- encode.rs:33-42 */
+size_t clay_encoded_chunk_size(const clay_code_t *code, size_t data_len);
+
+/* ------------------------------------------------------------------ */
+/* Host-buffer API (mirrors the reference semantics)                   */
+/* ------------------------------------------------------------------ */
+
+/* ClayCode::encode(data) -> Vec<Vec<u8>>   -- lib.rs:176-178, encode.rs:30-80.
+ * out_chunks: n host buffers of chunk_size bytes (chunk_size must equal
+ * clay_encoded_chunk_size(code, len)); [0,k) receive the zero-padded data
+ * chunks, [k,n) the parity chunks.  The reference panics on an internal error
+ * (encode.rs:67-68); this ABI returns CLAY_ERR_RECONSTRUCTION_FAILED instead. */
+int clay_encode(const clay_code_t *code, const uint8_t *data, size_t len,
+                uint8_t *const *out_chunks, size_t chunk_size, clay_error_t *err);
+
+/* ClayCode::decode(available, erasures) -> Vec<u8> -- lib.rs:188-194, decode.rs:31-161.
+ * available: n_avail entries (ids, bufs, lens).  out receives k*chunk bytes
+ * (the first k internal chunks, padding included, decode.rs:155-158);
+ * *out_len = k*chunk (0 for the empty/empty case).  out_cap < k*chunk ->
+ * CLAY_ERR_INVALID_PARAMETERS. */
+int clay_decode(const clay_code_t *code, const size_t *ids, const uint8_t *const *bufs,
+                const size_t *lens, size_t n_avail, const size_t *erasures, size_t n_erasures,
+                uint8_t *out, size_t out_cap, size_t *out_len, clay_error_t *err);
+
+/* ClayCode::minimum_to_repair(lost, available) -- lib.rs:207-213, repair.rs:61-126.
+ * Every helper needs the same sub-chunk list (repair.rs:102,113), so the result
+ * is helpers_out[0..*n_helpers) (capacity >= d) plus one index list
+ * subchunks_out[0..*n_subchunks) (capacity >= beta). */
+int clay_minimum_to_repair(const clay_code_t *code, size_t lost_node, const size_t *available,
+                           size_t n_available, size_t *helpers_out, size_t *n_helpers,
+                           size_t *subchunks_out, size_t *n_subchunks, clay_error_t *err);
+
+/* ClayCode::repair(lost, helper_data, chunk_size) -- lib.rs:226-233, repair.rs:140-421.
+ * helper i: ids[i], bufs[i] (lens[i] bytes = the beta sub-chunks concatenated in
+ * minimum_to_repair order).  out receives chunk_size bytes. */
+int clay_repair(const clay_code_t *code, size_t lost_node, const size_t *ids,
+                const uint8_t *const *bufs, const size_t *lens, size_t n_helpers,
+                size_t chunk_size, uint8_t *out, clay_error_t *err);
+
+/* ------------------------------------------------------------------ */
+/* Device-resident API (HBM in, HBM out; asynchronous on `stream`)      */
+/* ------------------------------------------------------------------ */
+
+/* Encode one stripe already resident in HBM.  data_chunks: k device pointers
+ * (chunk_size bytes each, chunk_size % sub_chunk_no == 0), parity_chunks: m
+ * device pointers.  Pointer arrays themselves are host memory.  Same bytes as
+ * clay_encode's parity for the same (padded) data.  stream: hipStream_t or NULL. */
+int clay_encode_device(const clay_code_t *code, const uint8_t *const *data_chunks,
+                       uint8_t *const *parity_chunks, size_t chunk_size, int device,
+                       void *stream, clay_error_t *err);
+
+/* Batched encode: `n_stripes` independent stripes, stripe s uses
+ * data_chunks[s*k .. s*k+k) and parity_chunks[s*m .. s*m+m). */
+int clay_encode_device_batch(const clay_code_t *code, const uint8_t *const *data_chunks,
+                             uint8_t *const *parity_chunks, size_t n_stripes, size_t chunk_size,
+                             int device, void *stream, clay_error_t *err);
+
+/* Decode / rebuild on device.  chunks: n device pointers, NULL for every erased
+ * node (validation as decode.rs:36-126 with available = the non-NULL entries).
+ * out_chunks: n device pointers; for every erased DATA node out_chunks[i] must
+ * be non-NULL and receives the rebuilt chunk; for an erased PARITY node a
+ * non-NULL out_chunks[i] also receives the rebuilt parity chunk (the value the
+ * reference computes internally, decode.rs:213-253); other entries are ignored. */
+int clay_decode_device(const clay_code_t *code, const uint8_t *const *chunks,
+                       const size_t *erasures, size_t n_erasures, uint8_t *const *out_chunks,
+                       size_t chunk_size, int device, void *stream, clay_error_t *err);
+
+/* Repair on device: helper buffers are device pointers (beta*sub-chunk bytes),
+ * out is a device buffer of chunk_size bytes. */
+int clay_repair_device(const clay_code_t *code, size_t lost_node, const size_t *helper_ids,
+                       const uint8_t *const *helper_bufs, size_t n_helpers, size_t chunk_size,
+                       uint8_t *out, int device, void *stream, clay_error_t *err);
+
+/* ------------------------------------------------------------------ */
+/* Engine control / introspection                                      */
+/* ------------------------------------------------------------------ */
+
+/* Pre-allocate per-device workspace for chunk_size (avoids allocation inside a
+ * later call, e.g. before stream capture). */
+int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int device,
+                           clay_error_t *err);
+
+/* Encode path selection: 0 = auto (fused kernel when the code shape allows it),
+ * 1 = force the generic staged engine, 2 = require the fused kernel (error if
+ * unsupported).  Process-wide; intended for tests and benchmarks. */
+int clay_set_encode_path(int mode);
+
+/* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
+const char *clay_last_encode_path(void);
+
+/* Number of kernel launches the last device call on this thread issued. */
+size_t clay_last_launch_count(void);
+
+/* Introspection (tests / tooling): export the staged-engine plan -- the
+ * reference's layered algorithm replayed into GF(2^8) region ops
+ * "dst = XOR coef*src" -- for kind 0 = encode, 1 = decode (mask = erased
+ * internal nodes, want = erased nodes whose C is wanted), 2 = repair (mask =
+ * helper internal nodes, lost = external lost node).  Records are uint32:
+ * ops_out[4*i..] = {dst_base, dst_slot, src_begin, nsrc}, srcs_out[4*j..] =
+ * {base, slot, coef, 0}, stages_out = stage begin offsets (n_stages+1).  Base
+ * index b: b < tn -> C[node b]; tn <= b < 2tn -> helper H[node b-tn]; 2tn -> U
+ * workspace (slot = node*alpha + z); 2tn+1 -> repaired chunk.  counts[] =
+ * {n_ops, n_srcs, n_stages+1}.  Capacities too small -> only counts filled. */
+int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, const uint8_t *want,
+                     size_t lost_node, uint32_t *ops_out, size_t ops_cap, uint32_t *srcs_out,
+                     size_t srcs_cap, uint32_t *stages_out, size_t stages_cap, size_t counts[3],
+                     clay_error_t *err);
+
+/* ABI version (CLAY_ABI_VERSION) and build string. */
+int clay_abi_version(void);
+const char *clay_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLAY_H */

@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU-box check: parity tests, smoke, bench, rocprof kernel stats.  Each GPU step
+# has its own time limit; steps are chained so the first failure ends the run.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$R" && mkdir -p gpurun_out
+TAG=${1:-run}
+echo "[$(date +%T)] pytest -m gpu (not slow)"
+timeout -k 10 600 python -m pytest tests -m "gpu and not slow" -x -q > gpurun_out/${TAG}_pytest_fast.log 2>&1 || { echo "pytest fast failed rc=$?"; tail -40 gpurun_out/${TAG}_pytest_fast.log; exit 1; }
+tail -3 gpurun_out/${TAG}_pytest_fast.log
+echo "[$(date +%T)] smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }
+tail -2 gpurun_out/${TAG}_smoke.log
+echo "[$(date +%T)] bench"
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/${TAG}_bench.log; exit 1; }
+tail -2 gpurun_out/${TAG}_bench.log
+echo "[$(date +%T)] rocprofv3 kernel trace"
+export TMPDIR=/tmp
+( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o enc --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-verify --no-host-path --cpu-seconds 0 ) > gpurun_out/${TAG}_rocprof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/${TAG}_rocprof.log; exit 1; }
+find gpurun_out/${TAG}_prof -name "*stats*" | head
+echo "[$(date +%T)] done"

@@ -1,0 +1,255 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit-exact.
+
+Small/medium sizes compare whole outputs with the oracle on the same seeded
+inputs; the BASELINE.json configurations run at full size (marked slow as well).
+Non-codeword (random) decode/repair inputs pin the reference's RS row selection.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+from clay_amd import ClayCode, set_encode_path, last_encode_path
+import clay_amd
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [(4, 2, 5), (6, 3, 8), (9, 3, 11), (10, 4, 13), (5, 3, 6), (7, 4, 9), (3, 3, 4), (8, 4, 11)]
+
+
+def rand_bytes(seed, n):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def internal(c, e):
+    return e if e < c.k else e + c.nu
+
+
+@pytest.fixture(autouse=True)
+def _auto_path():
+    set_encode_path("auto")
+    yield
+    set_encode_path("auto")
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+@pytest.mark.parametrize("size_kind", ["empty", "tiny", "ragged", "aligned16", "sc2"])
+def test_encode_matches_oracle(oracle_mod, cfg, size_kind):
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    unit = k * c.sub_chunk_no * 2
+    n = {"empty": 0, "tiny": 1, "ragged": unit * 3 + 17, "aligned16": unit * 8,
+         "sc2": unit * 5}[size_kind]
+    data = rand_bytes(hash(cfg) & 0xFFFF, n)
+    ref = o.encode_array(data)
+    got = c.encode_array(data)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref), (cfg, size_kind, clay_amd.last_encode_path())
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_encode_fused_equals_staged(oracle_mod, cfg):
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    data = rand_bytes(7, k * c.sub_chunk_no * 2 * 16 - 5)  # sc = 32: fused-eligible
+    ref = o.encode_array(data)
+    set_encode_path("staged")
+    a = c.encode_array(data)
+    assert last_encode_path() == "staged"
+    set_encode_path("auto")
+    b = c.encode_array(data)
+    assert np.array_equal(a, ref) and np.array_equal(b, ref), last_encode_path()
+    if c.q == c.m and c.q <= 4:
+        assert last_encode_path().startswith("fused"), last_encode_path()
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_decode_random_inputs_match_oracle(oracle_mod, cfg):
+    """Non-codeword inputs: only the reference's exact RS row choice reproduces these bytes."""
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    rng = np.random.default_rng(11)
+    chunk = c.sub_chunk_no * 6
+    pats = [list(e) for r in range(0, m + 1) for e in itertools.combinations(range(c.n), r)]
+    rng.shuffle(pats)
+    for er in pats[:12]:
+        chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+        av = {i: chunks[i] for i in range(c.n) if i not in er}
+        assert c.decode(av, er) == o.decode(av, er), (cfg, er)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_decode_roundtrip_max_erasures(oracle_mod, cfg):
+    k, m, d = cfg
+    c = ClayCode(k, m, d)
+    data = rand_bytes(3, k * c.sub_chunk_no * 4 + 9)
+    chunks = c.encode(data)
+    for er in list(itertools.combinations(range(c.n), m))[:20]:
+        av = {i: chunks[i] for i in range(c.n) if i not in er}
+        assert c.decode(av, list(er))[:len(data)] == data.tobytes(), (cfg, er)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_repair_every_node_matches_oracle(oracle_mod, cfg):
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    data = rand_bytes(5, k * c.sub_chunk_no * 2 * 3)
+    chunks = c.encode_array(data)
+    chunk = chunks.shape[1]
+    sc = chunk // c.sub_chunk_no
+    rng = np.random.default_rng(9)
+    for lost in range(c.n):
+        avail = [i for i in range(c.n) if i != lost]
+        info = c.minimum_to_repair(lost, avail)
+        assert info == o.minimum_to_repair(lost, avail)
+        pd = {h: np.concatenate([chunks[h][z * sc:(z + 1) * sc] for z in idx]) for h, idx in info}
+        rec = c.repair(lost, pd, chunk)
+        assert rec == chunks[lost].tobytes(), (cfg, lost)
+        # random helper payloads: byte-identical to the reference's repair arithmetic
+        pr = {h: rng.integers(0, 256, v.size, dtype=np.uint8) for h, v in pd.items()}
+        assert c.repair(lost, pr, chunk) == o.repair(lost, pr, chunk), (cfg, lost)
+
+
+def test_repair_with_all_helpers_and_aloof(oracle_mod):
+    """More than d helpers, and exactly d with an aloof node (repair.rs:248-255)."""
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    data = rand_bytes(21, 10 * 256 * 2 * 2)
+    ch = c.encode_array(data)
+    chunk = ch.shape[1]
+    sc = chunk // 256
+    for lost in (0, 5, 9, 10, 13):
+        idx = c.minimum_to_repair(lost, [i for i in range(14) if i != lost])[0][1]
+        for helpers in ([i for i in range(14) if i != lost],
+                        [h for h, _ in c.minimum_to_repair(lost, [i for i in range(14) if i != lost])]):
+            pd = {h: np.concatenate([ch[h][z * sc:(z + 1) * sc] for z in idx]) for h in helpers}
+            got = c.repair(lost, pd, chunk)
+            assert got == o.repair(lost, pd, chunk) == ch[lost].tobytes()
+
+
+def test_errors_mirror_reference(oracle_mod):
+    c = ClayCode(4, 2, 5)
+    ch = c.encode(bytes(range(128)))
+    with pytest.raises(clay_amd.TooManyErasures) as e:
+        c.decode({i: ch[i] for i in range(3, 6)}, [0, 1, 2])
+    assert e.value.fields[:2] == (2, 3)
+    bad = {i: ch[i] for i in range(1, 6)}
+    bad[5] = ch[5] + b"\0"
+    with pytest.raises((clay_amd.InconsistentChunkSizes, clay_amd.InvalidChunkSize)):
+        c.decode(bad, [0])
+    with pytest.raises(clay_amd.InvalidParameters, match="both"):
+        c.decode({i: ch[i] for i in range(6)}, [0])
+    with pytest.raises(clay_amd.InvalidParameters, match="Expected"):
+        c.decode({i: ch[i] for i in range(2, 6)}, [0])
+
+
+# ---------------------------------------------------------------------------
+# device-resident API (torch allocations; pointers through the C ABI)
+# ---------------------------------------------------------------------------
+def test_device_api_encode_decode_repair(oracle_mod, torch_cuda):
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    data = rand_bytes(31, 10 * 256 * 2 * 40)
+    ref = o.encode_array(data)
+    chunk = ref.shape[1]
+    dev = torch.from_numpy(ref[:10].copy()).cuda()
+    par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    c.encode_device([dev[i] for i in range(10)], [par[i] for i in range(4)], chunk, 0, stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(par.cpu().numpy(), ref[10:])
+    # batched
+    dev2 = torch.stack([dev, dev.flip(1)])
+    par2 = torch.zeros((2, 4, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device_batch([dev2[s, i] for s in range(2) for i in range(10)],
+                          [par2[s, i] for s in range(2) for i in range(4)], 2, chunk, 0, stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(par2[0].cpu().numpy(), ref[10:])
+    ref_flip = o.encode_array(np.ascontiguousarray(ref[:10, ::-1]).reshape(-1))
+    assert np.array_equal(par2[1].cpu().numpy(), ref_flip[10:])
+    # decode on device: erase {0,4,8,12}, rebuild data and parity 12
+    full = torch.from_numpy(ref.copy()).cuda()
+    er = [0, 4, 8, 12]
+    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                    [outs[i] if i in er else None for i in range(14)], chunk, 0, stream)
+    torch.cuda.synchronize()
+    for e in er:
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
+    # repair on device
+    sc = chunk // 256
+    info = c.minimum_to_repair(3, [i for i in range(14) if i != 3])
+    hb = [torch.from_numpy(np.concatenate([ref[h][z * sc:(z + 1) * sc] for z in idx])).cuda()
+          for h, idx in info]
+    out = torch.zeros(chunk, dtype=torch.uint8, device="cuda")
+    c.repair_device(3, [h for h, _ in info], hb, chunk, out, 0, stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref[3])
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configurations at full size
+# ---------------------------------------------------------------------------
+@pytest.mark.slow
+def test_cfg2_4_2_5_64MiB_encode_decode(oracle_mod):
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    data = rand_bytes(42, 64 << 20)
+    ref = o.encode_array(data)
+    got = c.encode_array(data)
+    assert np.array_equal(got, ref), clay_amd.last_encode_path()
+    av = {i: ref[i] for i in range(1, 6)}
+    assert c.decode(av, [0]) == o.decode(av, [0])
+
+
+@pytest.mark.slow
+def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    data = rand_bytes(42, 1 << 30)
+    chunk = c.encoded_chunk_size(data.size)
+    assert chunk == 107_374_592
+    ref = o.encode_array(data)
+    dev = torch.from_numpy(ref[:10].copy()).cuda()
+    par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device([dev[i] for i in range(10)], [par[i] for i in range(4)], chunk)
+    torch.cuda.synchronize()
+    assert clay_amd.last_encode_path().startswith("fused")
+    assert np.array_equal(par.cpu().numpy(), ref[10:])
+
+
+@pytest.mark.slow
+def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda):
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    rng = np.random.default_rng(5)
+    chunk = 107_374_592
+    er = [0, 4, 8, 12]
+    # non-codeword inputs: pins row selection at full size too
+    chunks = rng.integers(0, 256, (14, chunk), dtype=np.uint8)
+    av = {i: chunks[i] for i in range(14) if i not in er}
+    ref = np.frombuffer(o.decode(av, er), np.uint8).reshape(10, chunk)
+    full = torch.from_numpy(chunks).cuda()
+    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                    [outs[i] if i in er else None for i in range(14)], chunk)
+    torch.cuda.synchronize()
+    for e in (0, 4, 8):
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
+
+
+@pytest.mark.slow
+def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda):
+    torch = torch_cuda
+    c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
+    chunk = 268_435_458
+    sc = chunk // 81
+    rng = np.random.default_rng(8)
+    lost = 0
+    info = c.minimum_to_repair(lost, list(range(1, 12)))
+    assert len(info) == 11 and len(info[0][1]) == 27
+    pd = {h: rng.integers(0, 256, 27 * sc, dtype=np.uint8) for h, _ in info}
+    ref = np.frombuffer(o.repair(lost, pd, chunk), np.uint8)
+    hb = [torch.from_numpy(pd[h]).cuda() for h, _ in info]
+    out = torch.zeros(chunk, dtype=torch.uint8, device="cuda")
+    c.repair_device(lost, [h for h, _ in info], hb, chunk, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
