@@ -1,0 +1,651 @@
+// bitslice.hpp -- bit-sliced GF(2^8) fused encode for gfx950 (compile-time code constants).
+//
+// Representation: one lane owns 32 consecutive byte positions of a sub-chunk.  The
+// 32 bytes (8 dwords) are transposed into 8 bit-planes P[b] (bit i of P[b] = bit b of
+// byte sigma(i)); in that domain multiplication by a constant c is an 8x8 GF(2)
+// matrix, i.e. a fixed XOR network over planes, generated at compile time from the
+// Reed-Solomon generator of reed-solomon-erasure 6.0.0 (constexpr restatement of
+// vandermonde(total, data) * inv(top), gf256.hpp).  Gamma = 2 (transforms.rs:20) is
+// applied in the byte domain (SWAR xtime) before the transpose.
+//
+// Per y-section line (q nodes x q layers differing in digit y) and per column j,
+//   U[x] = C[x][z_j] + g * C[j][z_x]        (PRT, transforms.rs:42-55; x == j: red copy)
+//   V[p][z_j] += sum_x M[p][yq+x] * U[x]      (per-layer RS encode, decode.rs:386-404)
+// V lives in LDS as bit-planes for the whole tile; the parity y-section then applies
+//   C[x][z_j] = det^-1 (V[x][z_j] + g V[j][z_x]) (PFT, transforms.rs:108-125)
+// and transposes back to bytes.  Same linear map as the reference, so the bytes are
+// identical (GF(2^8) arithmetic is exact).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+#include <utility>
+
+namespace clay {
+namespace bs {
+
+// ---------------- constexpr GF(2^8), poly 0x11D ----------------
+constexpr uint8_t gm(uint8_t a, uint8_t b) {
+    uint8_t r = 0;
+    for (int i = 0; i < 8; i++) {
+        if (b & 1) r ^= a;
+        b >>= 1;
+        a = uint8_t((a << 1) ^ ((a & 0x80) ? 0x1D : 0));
+    }
+    return r;
+}
+constexpr uint8_t gpw(uint8_t a, int n) {
+    uint8_t r = 1;
+    for (int i = 0; i < n; i++) r = gm(r, a);
+    return r;
+}
+constexpr uint8_t ginv(uint8_t a) { return gpw(a, 254); }
+
+template <int K, int M>
+struct RsRows {
+    uint8_t g[M][K];
+};
+
+// Parity rows K..K+M-1 of vandermonde(K+M, K) * inv(vandermonde top K x K).
+template <int K, int M>
+constexpr RsRows<K, M> rs_rows() {
+    uint8_t a[K][K] = {}, inv[K][K] = {};
+    for (int r = 0; r < K; r++)
+        for (int c = 0; c < K; c++) {
+            a[r][c] = gpw(uint8_t(r), c);
+            inv[r][c] = r == c ? 1 : 0;
+        }
+    for (int c = 0; c < K; c++) {
+        int piv = c;
+        while (a[piv][c] == 0) piv++;
+        for (int j = 0; j < K; j++) {
+            uint8_t t = a[c][j];
+            a[c][j] = a[piv][j];
+            a[piv][j] = t;
+            t = inv[c][j];
+            inv[c][j] = inv[piv][j];
+            inv[piv][j] = t;
+        }
+        uint8_t s = ginv(a[c][c]);
+        for (int j = 0; j < K; j++) {
+            a[c][j] = gm(a[c][j], s);
+            inv[c][j] = gm(inv[c][j], s);
+        }
+        for (int r = 0; r < K; r++) {
+            if (r == c || a[r][c] == 0) continue;
+            uint8_t f = a[r][c];
+            for (int j = 0; j < K; j++) {
+                a[r][j] ^= gm(f, a[c][j]);
+                inv[r][j] ^= gm(f, inv[c][j]);
+            }
+        }
+    }
+    RsRows<K, M> out = {};
+    for (int p = 0; p < M; p++)
+        for (int c = 0; c < K; c++) {
+            uint8_t acc = 0;
+            for (int i = 0; i < K; i++) acc ^= gm(gpw(uint8_t(K + p), i), inv[i][c]);
+            out.g[p][c] = acc;
+        }
+    return out;
+}
+
+// ---------------- compile-time loops ----------------
+// Lambdas passed to sfor must inline completely (arrays captured by reference
+// would otherwise be demoted to scratch / LDS).
+#define BS_INL __attribute__((always_inline))
+template <class F, int... Is>
+__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------- bit-plane kernels ----------------
+// v_bitop3_b32 LUTs (inputs a=0xF0, b=0xCC, c=0xAA)
+constexpr unsigned kSel = 0xCA;   // a ? b : c
+constexpr unsigned kXor3 = 0x96;  // a ^ b ^ c
+constexpr unsigned kXorAnd = 0x78;  // a ^ (b & c)
+
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t x, uint32_t y) {
+    return __builtin_amdgcn_bitop3_b32(m, x, y, kSel);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, kXor3);
+}
+
+// 32 bytes (8 dwords, byte 4w+j at bits 8j..8j+7 of d[w]) <-> 8 bit-planes.
+// Three delta swaps exchange the dword-index bits with the bit-in-byte bits; the
+// map is an involution, so the same routine transposes back.
+template <int S, uint32_t MLO>
+__device__ __forceinline__ void swap_bits(uint32_t &a, uint32_t &b) {
+    const uint32_t na = sel(MLO, a, b << S);   // keep a's low half, take b's (shifted up)
+    const uint32_t nb = sel(MLO, a >> S, b);   // take a's high half (shifted down), keep b's
+    a = na;
+    b = nb;
+}
+__device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
+    swap_bits<1, 0x55555555u>(d[0], d[1]);
+    swap_bits<1, 0x55555555u>(d[2], d[3]);
+    swap_bits<1, 0x55555555u>(d[4], d[5]);
+    swap_bits<1, 0x55555555u>(d[6], d[7]);
+    swap_bits<2, 0x33333333u>(d[0], d[2]);
+    swap_bits<2, 0x33333333u>(d[1], d[3]);
+    swap_bits<2, 0x33333333u>(d[4], d[6]);
+    swap_bits<2, 0x33333333u>(d[5], d[7]);
+    swap_bits<4, 0x0F0F0F0Fu>(d[0], d[4]);
+    swap_bits<4, 0x0F0F0F0Fu>(d[1], d[5]);
+    swap_bits<4, 0x0F0F0F0Fu>(d[2], d[6]);
+    swap_bits<4, 0x0F0F0F0Fu>(d[3], d[7]);
+}
+
+// o ^ gamma*c on 4 packed bytes (xtime, poly 0x11D).  Byte-wise "top bit set" masks
+// come from v_perm_b32's sign-replicate selectors (8..11), avoiding a multiply.
+__device__ __forceinline__ uint32_t xor_xtime4(uint32_t o, uint32_t c) {
+    const uint32_t sh = (c << 1) & 0xfefefefeu;
+    const uint32_t m = __builtin_amdgcn_perm(c, c << 8, 0x0B090A08u);  // 0xFF where byte MSB set
+    return xor3(o, sh, m & 0x1d1d1d1du);
+}
+
+// o ^ (gamma*c if keep) with ks = keep & 0xfefefefe, kr = keep & 0x1d1d1d1d
+__device__ __forceinline__ uint32_t xor_xtime4_masked(uint32_t o, uint32_t c, uint32_t ks, uint32_t kr) {
+    const uint32_t m = __builtin_amdgcn_perm(c, c << 8, 0x0B090A08u);
+    const uint32_t t = __builtin_amdgcn_bitop3_b32(o, c << 1, ks, kXorAnd);  // o ^ ((c<<1) & ks)
+    return __builtin_amdgcn_bitop3_b32(t, m, kr, kXorAnd);                  // ^ (m & kr)
+}
+
+__device__ __forceinline__ void xt_planes(const uint32_t (&in)[8], uint32_t (&out)[8]) {
+    out[0] = in[7];
+    out[1] = in[0];
+    out[2] = in[1] ^ in[7];
+    out[3] = in[2] ^ in[7];
+    out[4] = in[3] ^ in[7];
+    out[5] = in[4];
+    out[6] = in[5];
+    out[7] = in[6];
+}
+
+constexpr int popc(uint64_t v) {
+    int n = 0;
+    for (; v; v &= v - 1) n++;
+    return n;
+}
+
+// acc (or 0 if !ACC) ^ XOR of in[i] over the set bits of MASK, as 3-input XOR chains.
+template <uint64_t MASK, bool ACC, int N>
+__device__ __forceinline__ uint32_t xor_sel(uint32_t acc, const uint32_t (&in)[N]) {
+    constexpr int total = popc(MASK);
+    if constexpr (total == 0) {
+        return ACC ? acc : 0u;
+    } else {
+        uint32_t pend = 0;
+        bool have = ACC;  // compile-time after unrolling
+        sfor<N>([&](auto ic) BS_INL {
+            constexpr int i = decltype(ic)::value;
+            if constexpr ((MASK >> i) & 1) {
+                constexpr int rank = popc(MASK & ((uint64_t(1) << i) - 1));
+                if constexpr (!ACC && rank == 0) {
+                    acc = in[i];
+                } else if constexpr ((rank + (ACC ? 1 : 0)) % 2 == 1 && rank != total - 1) {
+                    pend = in[i];
+                } else if constexpr ((rank + (ACC ? 1 : 0)) % 2 == 1) {
+                    acc ^= in[i];
+                } else {
+                    acc = xor3(acc, pend, in[i]);
+                }
+            }
+        });
+        (void)have;
+        return acc;
+    }
+}
+
+// GF(2^8) constant as an 8x8 bit matrix: column bi = C * 2^bi.
+constexpr uint64_t plane_mask(uint8_t c, int bo, int shift) {
+    uint64_t m = 0;
+    for (int bi = 0; bi < 8; bi++)
+        if ((gm(c, uint8_t(1u << bi)) >> bo) & 1) m |= uint64_t(1) << (bi + shift);
+    return m;
+}
+
+}  // namespace bs
+}  // namespace clay
+
+namespace clay {
+namespace bs {
+
+constexpr int kMaxNodes = 64;
+
+struct BsArgs {
+    const uint8_t *data[kMaxNodes];  // internal nodes 0..K-1 (nullptr: shortened, known zero)
+    uint8_t *par[8];                 // parity y-section, node x (internal (t-1)q + x)
+    uint64_t sc;                     // sub-chunk bytes, multiple of 8
+    uint32_t ntiles, tiles_per_xcd, nslots;
+};
+
+// Code shape derived at compile time from (k, m) with d = k + m - 1 (q = m).
+template <int KD, int M>
+struct Shape {
+    static constexpr int Q = M;
+    static constexpr int N = KD + M;
+    static constexpr int NU = (N % Q == 0) ? 0 : Q - N % Q;
+    static constexpr int T = (N + NU) / Q;
+    static constexpr int K = KD + NU;
+    static constexpr int ALPHA = [] { int a = 1; for (int i = 0; i < T; i++) a *= Q; return a; }();
+    static constexpr RsRows<K, M> RS = rs_rows<K, M>();
+    static constexpr uint8_t DINV = ginv(uint8_t(1 ^ gm(2, 2)));
+};
+
+template <int Q>
+__device__ __forceinline__ const uint8_t *pick(const uint8_t *const (&p)[Q], int i) {
+    const uint8_t *r = p[0];
+#pragma unroll
+    for (int x = 1; x < Q; x++) r = (i == x) ? p[x] : r;
+    return r;
+}
+
+// 32-byte lane load/store (four 8-byte pieces; in a partial tile only `nv` pieces exist)
+template <bool FULL>
+__device__ __forceinline__ void ld32(uint32_t (&d)[8], const uint8_t *p, int nv) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (FULL || i < nv) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(p + 8 * i);
+            d[2 * i] = v.x;
+            d[2 * i + 1] = v.y;
+        } else {
+            d[2 * i] = 0;
+            d[2 * i + 1] = 0;
+        }
+    }
+}
+template <bool FULL>
+__device__ __forceinline__ void st32(uint8_t *p, const uint32_t (&d)[8], int nv) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        if (FULL || i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
+}
+
+template <int KD, int M, int PG>
+struct BsKernel {
+    using S = Shape<KD, M>;
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA, UNITS = ALPHA * PG;
+    static constexpr int BLOCK = UNITS < 1024 ? UNITS : 1024;
+    static constexpr int W = 32 * PG;                          // positions per tile
+    static constexpr int LDS_WORDS = Q * ALPHA * PG * 8;       // parity-U planes
+
+    // RS parity row p over the q U-values of y-section Y, output plane bo:
+    // XOR of U[x][bi] where bit bo of M[p][Yq+x] * 2^bi is set (flat index x*8+bi).
+    template <int Y, int P, int BO>
+    static constexpr uint64_t rs_mask() {
+        uint64_t m = 0;
+        for (int x = 0; x < Q; x++) m |= plane_mask(S::RS.g[P][Y * Q + x], BO, 8 * x);
+        return m;
+    }
+    // PFT output plane bo: det^-1 * a + (det^-1 * gamma) * b over [a planes | b planes]
+    template <int BO>
+    static constexpr uint64_t pft_mask() {
+        return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
+    }
+
+    // ---- phase A, one y-section ----
+    template <int Y, bool FULL>
+    __device__ static void section(const BsArgs &a, uint32_t *lds, uint64_t b0) {
+        constexpr int WY = [] { int w = 1; for (int i = 0; i < T - 1 - Y; i++) w *= Q; return w; }();
+        for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
+            const int pg = u % PG, j = (u / PG) % Q, line = u / (PG * Q);
+            const int hi = line / WY, lo = line % WY;
+            const int zbase = hi * WY * Q + lo;
+            const uint64_t pos = b0 + uint64_t(32 * pg);
+            const int nv = FULL ? 4 : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);
+            const uint64_t lane_off = uint64_t(zbase) * a.sc + pos;
+            // companion node (Y, j); for j == x or a shortened companion the load is
+            // still issued (it hits lines a neighbour lane loads) and masked to zero
+            const bool creal = (Y * Q + j) < KD;
+            const uint8_t *cnode = a.data[creal ? Y * Q + j : Y * Q];
+            uint32_t U[Q * 8];
+            sfor<Q>([&](auto xc) BS_INL {
+                constexpr int x = decltype(xc)::value;
+                uint32_t o[8], c[8];
+                if constexpr (Y * Q + x < KD) {
+                    ld32<FULL>(o, a.data[Y * Q + x] + lane_off + uint64_t(j) * WY * a.sc, nv);
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) o[w] = 0;
+                }
+                ld32<FULL>(c, cnode + lane_off + uint64_t(x) * WY * a.sc, nv);
+                const uint32_t keep = (creal && x != j) ? 0xffffffffu : 0u;
+                const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                uint32_t t[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++) t[w] = xor_xtime4_masked(o[w], c[w], ks, kr);
+                transpose8(t);
+#pragma unroll
+                for (int w = 0; w < 8; w++) U[x * 8 + w] = t[w];
+            });
+            uint32_t *acc = lds + (size_t(zbase + j * WY) * PG + pg) * 8;
+            sfor<Q>([&](auto pc) BS_INL {
+                constexpr int p = decltype(pc)::value;
+                uint4 *l = reinterpret_cast<uint4 *>(acc + size_t(p) * ALPHA * PG * 8);
+                uint32_t V[8];
+                if constexpr (Y == 0) {
+                    sfor<8>([&](auto bc) BS_INL {
+                        V[decltype(bc)::value] = xor_sel<rs_mask<Y, p, decltype(bc)::value>(), false>(0u, U);
+                    });
+                } else {
+                    const uint4 v0 = l[0], v1 = l[1];
+                    V[0] = v0.x; V[1] = v0.y; V[2] = v0.z; V[3] = v0.w;
+                    V[4] = v1.x; V[5] = v1.y; V[6] = v1.z; V[7] = v1.w;
+                    sfor<8>([&](auto bc) BS_INL {
+                        V[decltype(bc)::value] = xor_sel<rs_mask<Y, p, decltype(bc)::value>(), true>(V[decltype(bc)::value], U);
+                    });
+                }
+                l[0] = make_uint4(V[0], V[1], V[2], V[3]);
+                l[1] = make_uint4(V[4], V[5], V[6], V[7]);
+            });
+        }
+    }
+
+    __device__ static void read8(const uint32_t *lds, int p, int z, int pg, uint32_t *v) {
+        const uint4 *l = reinterpret_cast<const uint4 *>(lds + ((size_t(p) * ALPHA + z) * PG + pg) * 8);
+        const uint4 v0 = l[0], v1 = l[1];
+        v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+        v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    }
+
+    // ---- phase B: PFT of the parity y-section (digit t-1, weight 1) + store ----
+    template <bool FULL>
+    __device__ static void finish(const BsArgs &a, const uint32_t *lds, uint64_t b0) {
+        for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
+            const int pg = u % PG, j = (u / PG) % Q, g = u / (PG * Q);
+            const int z0 = g * Q;
+            const uint64_t pos = b0 + uint64_t(32 * pg);
+            const int nv = FULL ? 4 : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);
+            const uint64_t off = uint64_t(z0 + j) * a.sc + pos;
+            {   // red vertex: C = U
+                uint32_t v[8];
+                read8(lds, j, z0 + j, pg, v);
+                transpose8(v);
+                st32<FULL>(a.par[j] + off, v, nv);
+            }
+#pragma unroll
+            for (int k = 1; k < Q; k++) {
+                const int x = (j + k) % Q;
+                uint32_t in[16], c[8];
+                read8(lds, x, z0 + j, pg, in);      // U at (x, z0+j)
+                read8(lds, j, z0 + x, pg, in + 8);  // U* at (j, z0+x)
+                sfor<8>([&](auto bc) BS_INL {
+                    c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
+                });
+                transpose8(c);
+                st32<FULL>(a.par[x] + off, c, nv);
+            }
+        }
+    }
+
+    template <bool FULL>
+    __device__ static void tile(const BsArgs &a, uint32_t *lds, uint64_t b0) {
+        sfor<T - 1>([&](auto yc) BS_INL {
+            section<decltype(yc)::value, FULL>(a, lds, b0);
+            __syncthreads();
+        });
+        finish<FULL>(a, lds, b0);
+        __syncthreads();
+    }
+};
+
+template <int KD, int M, int PG>
+__global__ __launch_bounds__((BsKernel<KD, M, PG>::BLOCK)) void k_bs_encode(BsArgs a) {
+    using Kn = BsKernel<KD, M, PG>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Kn::LDS_WORDS];
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    for (uint32_t tix = slot; tix < a.tiles_per_xcd; tix += a.nslots) {
+        const uint32_t tile = xcd * a.tiles_per_xcd + tix;
+        if (tile >= a.ntiles) break;
+        const uint64_t b0 = uint64_t(tile) * Kn::W;
+        if (b0 + Kn::W <= a.sc) Kn::template tile<true>(a, lds, b0);
+        else Kn::template tile<false>(a, lds, b0);
+    }
+}
+
+}  // namespace bs
+}  // namespace clay
+
+namespace clay {
+namespace bs {
+
+// ===========================================================================
+// v2: wave-private LDS staging with LDS-DMA prefetch.
+//
+// Wave w owns lines [L*w, L*w + L) of every y-section (L = 64 lanes / (q*PG)).  It
+// stages its lines' q*q values (node x, column jj) x W bytes into a private LDS
+// region with global_load_lds (coalesced 16-lane x 4 B = 64 B segments; every byte
+// read from HBM once; companions come from LDS).  As soon as the wave has pulled a
+// stage into registers it issues the DMA for its next section (or the next tile's
+// first section), so HBM latency overlaps the XOR networks, the accumulate, the
+// section barrier and the PFT.  Barriers are raw s_barrier + lgkmcnt(0) so the DMA
+// stays in flight across them.
+// ===========================================================================
+// LDS-DMA (global_load_lds_dword) issued from inline asm: LDS dest = M0 + lane*4,
+// global = sbase (SGPR pair) + voff (per-lane 32-bit).  Hidden from the compiler's
+// waitcnt pass on purpose (it would otherwise drain vmcnt before every LDS access);
+// the kernel waits for it explicitly with wait_vm0().
+__device__ __forceinline__ void dma4(uint32_t lds_addr, const uint8_t *sbase, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n" ::"s"(lds_addr), "v"(voff),
+                 "s"(sbase)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr_of(const void *p) {
+    return uint32_t(size_t((__attribute__((address_space(3))) const uint8_t *)(p)));
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int KD, int M>
+struct Bs2Kernel {
+    using S = Shape<KD, M>;
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
+    static constexpr int PG = 2;                       // lanes per value (32 positions each)
+    static constexpr int W = 32 * PG;                  // 64 positions per tile
+    static constexpr int LPW = 64 / (Q * PG);          // lines per wave
+    static_assert(Q == 4, "v2 staging assumes q == 4 (uniform node per DMA instruction)");
+    static constexpr int LINES = ALPHA / Q;            // lines per section
+    static constexpr int WAVES = LINES / LPW;
+    static constexpr int BLOCK = 64 * WAVES;
+    static_assert(LINES % LPW == 0 && BLOCK <= 1024, "shape");
+    static constexpr int ACC_WORDS = Q * ALPHA * PG * 8;
+    static constexpr int STAGE_BYTES = LPW * Q * Q * W;      // per wave
+    static constexpr int LDS_BYTES = ACC_WORDS * 4 + WAVES * STAGE_BYTES;
+    static constexpr int DMA_PER_SECTION = STAGE_BYTES / 256;  // 64 lanes x 4 B per instruction
+
+    template <int Y>
+    static constexpr int wy() { int w = 1; for (int i = 0; i < T - 1 - Y; i++) w *= Q; return w; }
+
+    // Issue the wave's DMA for section Y of the tile starting at b0.
+    // Value v = (line_local, x, jj) flattened as (line_local*Q + x)*Q + jj; one
+    // instruction stages 4 values (16 lanes x 4 B each): with Q == 4 the node x and
+    // the line are uniform per instruction (SGPR base), the column jj = lane/16
+    // and the byte offset live in a 32-bit per-lane offset computed once.
+    template <int Y>
+    __device__ static void dma(const BsArgs &a, uint32_t stage_lds, int wave, int lane, uint64_t b0) {
+        constexpr int WY = wy<Y>();
+        uint64_t pos = b0 + uint64_t(lane & 15) * 4;
+        if (pos + 4 > a.sc) pos = 0;  // ragged last tile: any valid bytes (never stored)
+        const uint32_t voff = uint32_t(uint64_t(lane >> 4) * WY * a.sc + pos);
+#pragma unroll
+        for (int i = 0; i < DMA_PER_SECTION; i++) {
+            const int x = i % Q, ll = i / Q;
+            const int node = Y * Q + x;
+            if (node >= KD) continue;  // shortened node: known zero, never read
+            const int line = wave * LPW + ll;
+            const uint64_t zl = uint64_t((line / WY) * WY * Q + (line % WY));
+            dma4(stage_lds + uint32_t(i) * 256u, a.data[node] + zl * a.sc, voff);
+        }
+    }
+
+    __device__ static void read32(const uint8_t *p, uint32_t (&d)[8]) {
+        const uint4 v0 = reinterpret_cast<const uint4 *>(p)[0], v1 = reinterpret_cast<const uint4 *>(p)[1];
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+
+    template <int Y, int P, int BO>
+    static constexpr uint64_t rs_mask() {
+        uint64_t m = 0;
+        for (int x = 0; x < Q; x++) m |= plane_mask(S::RS.g[P][Y * Q + x], BO, 8 * x);
+        return m;
+    }
+    template <int BO>
+    static constexpr uint64_t pft_mask() {
+        return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
+    }
+
+    // Section Y: stage -> registers, prefetch the next DMA, XOR networks, accumulate.
+    template <int Y>
+    __device__ static void section(const BsArgs &a, uint32_t *acc, uint8_t *stage, int wave, int lane,
+                                   uint64_t b0, uint64_t next_b0, bool has_next) {
+        constexpr int WY = wy<Y>();
+        const int pg = lane % PG, j = (lane / PG) % Q, ll = lane / (PG * Q);
+        const int line = wave * LPW + ll;
+        const int zj = (line / WY) * WY * Q + (line % WY) + j * WY;
+        const bool creal = (Y * Q + j) < KD;
+        wait_vm0();  // this wave's DMA for section Y has landed
+        uint32_t U[Q * 8];
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t o[8], c[8];
+            if constexpr (Y * Q + x < KD) {
+                read32(stage + ((ll * Q + x) * Q + j) * W + pg * 32, o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) o[w] = 0;
+            }
+            read32(stage + ((ll * Q + j) * Q + x) * W + pg * 32, c);
+            const uint32_t keep = (creal && x != j) ? 0xffffffffu : 0u;
+            const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+#pragma unroll
+            for (int w = 0; w < 8; w++) U[x * 8 + w] = xor_xtime4_masked(o[w], c[w], ks, kr);
+        });
+        // every lane of the wave has its stage values in registers -> refill the stage
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (Y + 1 < T - 1) {
+            dma<Y + 1>(a, lds_addr_of(stage), wave, lane, b0);
+        } else {
+            if (has_next) dma<0>(a, lds_addr_of(stage), wave, lane, next_b0);
+        }
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t t[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) t[w] = U[x * 8 + w];
+            transpose8(t);
+#pragma unroll
+            for (int w = 0; w < 8; w++) U[x * 8 + w] = t[w];
+        });
+        uint32_t *accp = acc + (size_t(zj) * PG + pg) * 8;
+        sfor<Q>([&](auto pc) BS_INL {
+            constexpr int p = decltype(pc)::value;
+            uint4 *l = reinterpret_cast<uint4 *>(accp + size_t(p) * ALPHA * PG * 8);
+            uint32_t V[8];
+            if constexpr (Y == 0) {
+                sfor<8>([&](auto bc) BS_INL {
+                    V[decltype(bc)::value] = xor_sel<rs_mask<Y, p, decltype(bc)::value>(), false>(0u, U);
+                });
+            } else {
+                const uint4 v0 = l[0], v1 = l[1];
+                V[0] = v0.x; V[1] = v0.y; V[2] = v0.z; V[3] = v0.w;
+                V[4] = v1.x; V[5] = v1.y; V[6] = v1.z; V[7] = v1.w;
+                sfor<8>([&](auto bc) BS_INL {
+                    V[decltype(bc)::value] = xor_sel<rs_mask<Y, p, decltype(bc)::value>(), true>(V[decltype(bc)::value], U);
+                });
+            }
+            l[0] = make_uint4(V[0], V[1], V[2], V[3]);
+            l[1] = make_uint4(V[4], V[5], V[6], V[7]);
+        });
+    }
+
+    __device__ static void read_acc(const uint32_t *acc, int p, int z, int pg, uint32_t *v) {
+        const uint4 *l = reinterpret_cast<const uint4 *>(acc + ((size_t(p) * ALPHA + z) * PG + pg) * 8);
+        const uint4 v0 = l[0], v1 = l[1];
+        v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+        v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    }
+
+    __device__ static void store32(uint8_t *p, const uint32_t (&d)[8], int nv) {
+        if (nv >= 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
+        }
+    }
+
+    // PFT of the parity y-section (digit t-1, weight 1) for this wave's groups + store.
+    __device__ static void finish(const BsArgs &a, const uint32_t *acc, int wave, int lane, uint64_t b0) {
+        const int pg = lane % PG, j = (lane / PG) % Q, gl = lane / (PG * Q);
+        const int z0 = (wave * LPW + gl) * Q;
+        const uint64_t pos = b0 + uint64_t(32 * pg);
+        const int nv = pos >= a.sc ? 0 : ((a.sc - pos) / 8 > 4 ? 4 : int((a.sc - pos) / 8));
+        const uint64_t off = uint64_t(z0 + j) * a.sc + pos;
+        {
+            uint32_t v[8];
+            read_acc(acc, j, z0 + j, pg, v);
+            transpose8(v);
+            store32(a.par[j] + off, v, nv);
+        }
+#pragma unroll
+        for (int k = 1; k < Q; k++) {
+            const int x = (j + k) % Q;
+            uint32_t in[16], c[8];
+            read_acc(acc, x, z0 + j, pg, in);
+            read_acc(acc, j, z0 + x, pg, in + 8);
+            sfor<8>([&](auto bc) BS_INL {
+                c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
+            });
+            transpose8(c);
+            store32(a.par[x] + off, c, nv);
+        }
+    }
+};
+
+template <int KD, int M>
+__global__ __launch_bounds__((Bs2Kernel<KD, M>::BLOCK)) void k_bs2_encode(BsArgs a) {
+    using Kn = Bs2Kernel<KD, M>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t *acc = reinterpret_cast<uint32_t *>(smem);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    uint8_t *stage = smem + Kn::ACC_WORDS * 4 + wave * Kn::STAGE_BYTES;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    uint32_t tix = slot;
+    uint32_t tile = xcd * a.tiles_per_xcd + tix;
+    if (tix >= a.tiles_per_xcd || tile >= a.ntiles) return;
+    Kn::template dma<0>(a, lds_addr_of(stage), wave, lane, uint64_t(tile) * Kn::W);
+    while (true) {
+        const uint64_t b0 = uint64_t(tile) * Kn::W;
+        const uint32_t ntix = tix + a.nslots, ntile = xcd * a.tiles_per_xcd + ntix;
+        const bool has_next = ntix < a.tiles_per_xcd && ntile < a.ntiles;
+        const uint64_t nb0 = uint64_t(ntile) * Kn::W;
+        sfor<Kn::T - 1>([&](auto yc) BS_INL {
+            Kn::template section<decltype(yc)::value>(a, acc, stage, wave, lane, b0, nb0, has_next);
+            lds_barrier();
+        });
+        Kn::finish(a, acc, wave, lane, b0);
+        lds_barrier();
+        if (!has_next) break;
+        tix = ntix;
+        tile = ntile;
+    }
+    wait_vm0();
+}
+
+}  // namespace bs
+}  // namespace clay

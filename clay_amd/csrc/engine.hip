@@ -27,6 +27,7 @@
 #include "../../include/clay.h"
 #include "code.hpp"
 #include "gf256.hpp"
+#include "bitslice.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -237,6 +238,7 @@ static std::mutex g_mu;
 static thread_local std::string t_last_path = "none";
 static thread_local size_t t_last_launches = 0;
 static int g_encode_mode = 0;
+static int g_bs_pg = 0;  // bit-sliced tile width override (lanes of 32 positions); 0 = default
 
 struct Workspace {
     void *ptr = nullptr;
@@ -488,6 +490,120 @@ static Error encode_fused(CodeState &cs, DevState &ds, int dev, const uint8_t *c
     return Error{};
 }
 
+// ---------------------------------------------------------------------------
+// Bit-sliced fused encode (bitslice.hpp): compile-time instantiations per code.
+// ---------------------------------------------------------------------------
+template <int KD, int M, int PG>
+static Error launch_bs(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
+                       size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::BsKernel<KD, M, PG>;
+    using S = typename Kn::S;
+    const clay_code_t &c = cs.code;
+    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
+    // the compile-time generator must equal the run-time one (same construction)
+    for (int p = 0; p < M; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    const int per_cu = std::max(1, int((160 * 1024) / (Kn::LDS_WORDS * 4)));
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::BsArgs a{};
+        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
+        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
+        a.sc = sc;
+        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
+        a.tiles_per_xcd = (a.ntiles + 7) / 8;
+        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
+        a.nslots = std::min(max_slots, a.tiles_per_xcd);
+        bs::k_bs_encode<KD, M, PG><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+        CLAY_HIP(hipGetLastError());
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "bitsliced-k%dm%d-w%d", KD, M, Kn::W);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
+template <int KD, int M>
+static Error launch_bs2(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
+                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::Bs2Kernel<KD, M>;
+    using S = typename Kn::S;
+    const clay_code_t &c = cs.code;
+    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
+    // per-lane DMA offsets are 32-bit: (q-1) * q^(t-2) * sc + sc must fit
+    if (double(M - 1) * double(S::ALPHA / M) * double(sc) + double(sc) >= 4294967296.0) return Error{};
+    for (int p = 0; p < M; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    static bool attr[64] = {};
+    int dev = 0;
+    CLAY_HIP(hipGetDevice(&dev));
+    if (!attr[dev]) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs2_encode<KD, M>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
+        attr[dev] = true;
+    }
+    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::BsArgs a{};
+        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
+        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
+        a.sc = sc;
+        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
+        a.tiles_per_xcd = (a.ntiles + 7) / 8;
+        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
+        a.nslots = std::min(max_slots, a.tiles_per_xcd);
+        bs::k_bs2_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        CLAY_HIP(hipGetLastError());
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "bitsliced2-k%dm%d-w%d", KD, M, Kn::W);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
+static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data, uint8_t *const *par,
+                              size_t n_stripes, size_t chunk, hipStream_t stream, bool *done) {
+    *done = false;
+    const clay_code_t &c = cs.code;
+    const size_t sc = chunk / c.sub_chunk_no;
+    if (sc % 8 != 0 || c.d != c.k + c.m - 1) return Error{};
+    for (size_t s = 0; s < n_stripes; s++) {
+        for (size_t i = 0; i < c.k; i++)
+            if (reinterpret_cast<uintptr_t>(data[s * c.k + i]) % 8) return Error{};
+        for (size_t i = 0; i < c.m; i++)
+            if (reinterpret_cast<uintptr_t>(par[s * c.m + i]) % 8) return Error{};
+    }
+    hipDeviceProp_t prop;
+    CLAY_HIP(hipGetDeviceProperties(&prop, dev));
+    Error e;
+    const int key = int(c.k * 100 + c.m);
+    if (g_encode_mode != 3 && (g_bs_pg == 0 || g_encode_mode == 4)) {  // v2 (LDS-DMA staged) first
+        if (key == 1004) e = launch_bs2<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+        else if (key == 804) e = launch_bs2<8, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+        if (e || *done || g_encode_mode == 4) return e;
+    }
+    switch (key) {
+    case 1004:
+        if (g_bs_pg == 1) e = launch_bs<10, 4, 1>(cs, prop, data, par, n_stripes, sc, stream, done);
+        else if (g_bs_pg == 4) e = launch_bs<10, 4, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+        else e = launch_bs<10, 4, 2>(cs, prop, data, par, n_stripes, sc, stream, done);
+        break;
+    case 402: e = launch_bs<4, 2, 64>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+    case 804: e = launch_bs<8, 4, 8>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+    case 903: e = launch_bs<9, 3, 6>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+    case 603: e = launch_bs<6, 3, 16>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+    default: break;
+    }
+    return e;
+}
+
 static Error encode_staged(CodeState &cs, DevState &ds, int dev, const uint8_t *const *data, uint8_t *const *par,
                            size_t n_stripes, size_t chunk, hipStream_t stream) {
     const clay_code_t &c = cs.code;
@@ -532,7 +648,14 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
         return make_error(CLAY_ERR_RECONSTRUCTION_FAILED, 0, 0, 0, "RS reconstruction failed: RS init failed: %s",
                           rs_error_name(cs.rs.init_err));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (g_encode_mode != 1) {
+    if (g_encode_mode == 0 || g_encode_mode == 3 || g_encode_mode == 4) {
+        bool done = false;
+        e = encode_bitsliced(cs, dev, data, par, n_stripes, chunk, st, &done);
+        if (e || done) return e;
+        if (g_encode_mode == 3 || g_encode_mode == 4)
+            return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced encode kernel does not support this code/alignment");
+    }
+    if (g_encode_mode == 0 || g_encode_mode == 2) {
         bool done = false;
         e = encode_fused(cs, *ds, dev, data, par, n_stripes, chunk, st, &done);
         if (e || done) return e;
@@ -682,7 +805,8 @@ const char *clay_build_info(void) { return "clay_amd " __DATE__ " gfx950 HIP"; }
 int clay_set_encode_path(int mode) {
     std::lock_guard<std::mutex> lk(g_mu);
     int prev = g_encode_mode;
-    g_encode_mode = mode;
+    g_encode_mode = mode & 0xFF;
+    g_bs_pg = (mode >> 8) & 0xFF;
     return prev;
 }
 const char *clay_last_encode_path(void) { return t_last_path.c_str(); }

@@ -161,9 +161,12 @@ int clay_repair_device(const clay_code_t *code, size_t lost_node, const size_t *
 int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int device,
                            clay_error_t *err);
 
-/* Encode path selection: 0 = auto (fused kernel when the code shape allows it),
- * 1 = force the generic staged engine, 2 = require the fused kernel (error if
- * unsupported).  Process-wide; intended for tests and benchmarks. */
+/* Encode path selection (process-wide; tests and benchmarks): low byte 0 = auto
+ * (bit-sliced kernel if the code has a compiled instantiation and sub-chunks are
+ * 8-byte aligned, else the byte-sliced fused kernel when parity is one y-section,
+ * else the staged engine), 1 = force staged, 2 = require byte-sliced fused,
+ * 3 = require bit-sliced.  Bits 8..15: bit-sliced tile override (0 = default).
+ * Returns the previous low-byte mode. */
 int clay_set_encode_path(int mode);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */

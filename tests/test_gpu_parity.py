@@ -33,18 +33,55 @@ def _auto_path():
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-@pytest.mark.parametrize("size_kind", ["empty", "tiny", "ragged", "aligned16", "sc2"])
+@pytest.mark.parametrize("size_kind", ["empty", "tiny", "ragged", "aligned16", "sc2", "big"])
 def test_encode_matches_oracle(oracle_mod, cfg, size_kind):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     unit = k * c.sub_chunk_no * 2
     n = {"empty": 0, "tiny": 1, "ragged": unit * 3 + 17, "aligned16": unit * 8,
-         "sc2": unit * 5}[size_kind]
+         "sc2": unit * 5, "big": unit * 40 - 3}[size_kind]
     data = rand_bytes(hash(cfg) & 0xFFFF, n)
     ref = o.encode_array(data)
     got = c.encode_array(data)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref), (cfg, size_kind, clay_amd.last_encode_path())
+
+
+BS_CODES = [(10, 4, 13), (4, 2, 5), (8, 4, 11), (9, 3, 11), (6, 3, 8)]
+
+
+@pytest.mark.parametrize("cfg", BS_CODES)
+@pytest.mark.parametrize("tile", [0, 1, 4])
+@pytest.mark.parametrize("scale", [1, 3, 37])
+def test_bitsliced_encode_matches_oracle(oracle_mod, cfg, tile, scale):
+    """Bit-sliced kernel: full tiles, the ragged last tile, every tile width."""
+    if tile and cfg != (10, 4, 13):
+        pytest.skip("tile override only instantiated for (10,4,13)")
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    n = k * c.sub_chunk_no * 8 * scale * 4 - 11  # sc = 32*scale: several tiles + a partial one
+    data = rand_bytes(scale * 7 + tile, n)
+    ref = o.encode_array(data)
+    set_encode_path("bitsliced", tile)
+    got = c.encode_array(data)
+    assert last_encode_path().startswith("bitsliced"), last_encode_path()
+    assert np.array_equal(got, ref), (cfg, tile, scale)
+
+
+@pytest.mark.parametrize("cfg", [(10, 4, 13), (8, 4, 11)])
+@pytest.mark.parametrize("scale", [1, 2, 3, 37, 200])
+def test_bitsliced2_encode_matches_oracle(oracle_mod, cfg, scale):
+    """LDS-DMA staged bit-sliced kernel: single/multiple tiles, ragged last tile,
+    and more tiles than workgroups (persistent loop + cross-tile prefetch)."""
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    n = k * c.sub_chunk_no * 8 * scale * 4 - 11
+    data = rand_bytes(scale * 13, n)
+    ref = o.encode_array(data)
+    set_encode_path("bitsliced2")
+    got = c.encode_array(data)
+    assert last_encode_path().startswith("bitsliced2"), last_encode_path()
+    assert np.array_equal(got, ref), (cfg, scale)
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
@@ -56,11 +93,13 @@ def test_encode_fused_equals_staged(oracle_mod, cfg):
     set_encode_path("staged")
     a = c.encode_array(data)
     assert last_encode_path() == "staged"
-    set_encode_path("auto")
+    set_encode_path("fused" if (c.q == c.m and c.q <= 4) else "auto")
     b = c.encode_array(data)
     assert np.array_equal(a, ref) and np.array_equal(b, ref), last_encode_path()
     if c.q == c.m and c.q <= 4:
         assert last_encode_path().startswith("fused"), last_encode_path()
+    set_encode_path("auto")
+    assert np.array_equal(c.encode_array(data), ref), last_encode_path()
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
