@@ -434,9 +434,17 @@ namespace bs {
 // waitcnt pass on purpose (it would otherwise drain vmcnt before every LDS access);
 // the kernel waits for it explicitly with wait_vm0().
 __device__ __forceinline__ void dma4(uint32_t lds_addr, const uint8_t *sbase, uint32_t voff) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n" ::"s"(lds_addr), "v"(voff),
-                 "s"(sbase)
-                 : "memory", "m0");
+    unsigned keep;  // M0 is compiler-reserved: save / restore it in the same statement
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, %3\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(lds_addr), "v"(voff), "s"(sbase)
+                 : "memory");
+}
+// 8-byte store issued from asm: exactly one VMEM instruction (never merged or
+// split by the compiler), so counted vmcnt waits stay exact.
+__device__ __forceinline__ void st8(uint8_t *p, uint32_t lo, uint32_t hi) {
+    const uint64_t v = uint64_t(lo) | (uint64_t(hi) << 32);
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ uint32_t lds_addr_of(const void *p) {
     return uint32_t(size_t((__attribute__((address_space(3))) const uint8_t *)(p)));
@@ -645,6 +653,286 @@ __global__ __launch_bounds__((Bs2Kernel<KD, M>::BLOCK)) void k_bs2_encode(BsArgs
         tile = ntile;
     }
     wait_vm0();
+}
+
+}  // namespace bs
+}  // namespace clay
+
+namespace clay {
+namespace bs {
+
+// ===========================================================================
+// v3: layer-per-lane, register accumulators, 2-slot section ring in LDS.
+//
+// Lane (layer z, half pg) accumulates V[p][z] = sum over the data y-sections of
+// M[p][yq+x] * U_y[x][z] in registers: every (line, column) step of the
+// reference's per-layer loop is exactly one (layer, section) pair, so nothing is
+// recomputed and no accumulator lives in LDS.  A section (q nodes x alpha layers x
+// W bytes) is staged by coalesced LDS-DMA two sections ahead in a 2-slot ring
+// shared by the workgroup; waits are counted s_waitcnt vmcnt so the next fill stays
+// in flight.  The PFT partners of the parity y-section (layers differing in the
+// last digit) form a lane quad and exchange through DPP.
+// ===========================================================================
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wave-uniform run-time count -> immediate
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+#define CLAY_VMW(k) case k: wait_vm_n<k>(); break;
+        CLAY_VMW(0) CLAY_VMW(1) CLAY_VMW(2) CLAY_VMW(4) CLAY_VMW(8) CLAY_VMW(12) CLAY_VMW(16)
+        CLAY_VMW(20) CLAY_VMW(24) CLAY_VMW(28) CLAY_VMW(32) CLAY_VMW(36) CLAY_VMW(40) CLAY_VMW(44)
+        CLAY_VMW(48) CLAY_VMW(52) CLAY_VMW(56) CLAY_VMW(60)
+#undef CLAY_VMW
+        default: wait_vm_n<0>(); break;  // conservative
+    }
+}
+
+template <int KD, int M>
+struct Bs3Kernel {
+    using S = Shape<KD, M>;
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA, NSEC = T - 1;
+    static_assert(Q == 4, "v3 assumes q == 4 (lane quads, uniform DMA node)");
+    static_assert(NSEC >= 2, "2-slot ring needs >= 2 data y-sections");
+    static constexpr int PG = 2, W = 64;
+    static constexpr int BLOCK = ALPHA * PG;  // one lane per (layer, half)
+    static_assert(BLOCK <= 1024 && BLOCK % 64 == 0, "shape");
+    static constexpr int WAVES = BLOCK / 64;
+    static_assert(WAVES % Q == 0, "each wave fills one node");
+    static constexpr int SLOT_BYTES = Q * ALPHA * W;               // one section, all layers
+    static constexpr int LDS_BYTES = 2 * SLOT_BYTES;
+    static constexpr int INSTR_PER_SLOT = SLOT_BYTES / 256;        // 256 B per DMA instruction
+    static constexpr int INSTR_PER_WAVE = INSTR_PER_SLOT / WAVES;
+    static constexpr int STORES_PER_TILE = Q * 4;                  // 4 outputs x 4 pieces of 8 B
+
+    template <int Y>
+    static constexpr int wy() { int w = 1; for (int i = 0; i < T - 1 - Y; i++) w *= Q; return w; }
+
+    // DMA instructions wave `wave` issues for section y (its node may be shortened)
+    __device__ static int n_dma(int y, int wave) { return (y * Q + wave % Q) < KD ? INSTR_PER_WAVE : 0; }
+
+    // Fill a slot with section Y of the tile at b0.  Instruction k covers node
+    // x = k % Q, layers [4(k/Q), 4(k/Q)+4); slot layout [x][z][W].  Wave w issues
+    // k = w + WAVES*i, so its node x = w % Q is uniform.
+    template <int Y>
+    __device__ static void dma(const BsArgs &a, uint32_t slot_lds, int wave, int lane, uint64_t b0) {
+        const int x = wave % Q;
+        if (Y * Q + x >= KD) return;  // shortened node: never staged, never read
+        uint64_t pos = b0 + uint64_t(lane & 15) * 4;
+        if (pos + 4 > a.sc) pos = 0;  // ragged last tile: any valid bytes (never stored)
+        const uint32_t voff = uint32_t(uint64_t(lane >> 4) * a.sc + pos);
+        const uint8_t *nb = a.data[Y * Q + x];
+#pragma unroll
+        for (int i = 0; i < INSTR_PER_WAVE; i++) {
+            const int k = wave + WAVES * i;
+            const int zb = 4 * (k / Q);
+            dma4(slot_lds + uint32_t((x * ALPHA + zb) * W), nb + uint64_t(zb) * a.sc, voff);
+        }
+    }
+    template <int Y>
+    __device__ static void dma_sec(int y, const BsArgs &a, uint32_t slot_lds, int wave, int lane, uint64_t b0) {
+        if constexpr (Y < NSEC) {
+            if (y == Y) dma<Y>(a, slot_lds, wave, lane, b0);
+            else dma_sec<Y + 1>(y, a, slot_lds, wave, lane, b0);
+        }
+    }
+
+    __device__ static void rd32(const uint8_t *p, uint32_t (&d)[8]) {
+        const uint4 v0 = reinterpret_cast<const uint4 *>(p)[0], v1 = reinterpret_cast<const uint4 *>(p)[1];
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+
+    template <int Y, int P, int BO>
+    static constexpr uint64_t rs_mask() {
+        uint64_t m = 0;
+        for (int x = 0; x < Q; x++) m |= plane_mask(S::RS.g[P][Y * Q + x], BO, 8 * x);
+        return m;
+    }
+    template <int BO>
+    static constexpr uint64_t pft_mask() {
+        return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
+    }
+
+    // Section Y: gather this lane's column (own C[x][z]; companion node (Y,d) at
+    // z + (x-d)*WY, d = digit Y of z) and apply the PRT in the byte domain.
+    template <int Y>
+    __device__ static void gather(const uint8_t *slot, int z, int pg, uint32_t (&U)[Q * 8]) {
+        constexpr int WY = wy<Y>();
+        const int d = (z / WY) % Q;
+        const bool creal = (Y * Q + d) < KD;
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t o[8], c[8];
+            if constexpr (Y * Q + x < KD) {
+                rd32(slot + (x * ALPHA + z) * W + pg * 32, o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) o[w] = 0;
+            }
+            rd32(slot + (d * ALPHA + z + (x - d) * WY) * W + pg * 32, c);
+            const uint32_t keep = (creal && x != d) ? 0xffffffffu : 0u;
+            const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+#pragma unroll
+            for (int w = 0; w < 8; w++) U[x * 8 + w] = xor_xtime4_masked(o[w], c[w], ks, kr);
+        });
+    }
+    // bit-slice the U column and add the section's RS contribution into V
+    template <int Y>
+    __device__ static void accumulate(uint32_t (&U)[Q * 8], uint32_t (&V)[Q][8]) {
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t t[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) t[w] = U[x * 8 + w];
+            transpose8(t);
+#pragma unroll
+            for (int w = 0; w < 8; w++) U[x * 8 + w] = t[w];
+        });
+        sfor<Q>([&](auto pc) BS_INL {
+            constexpr int p = decltype(pc)::value;
+            sfor<8>([&](auto bc) BS_INL {
+                constexpr int bo = decltype(bc)::value;
+                V[p][bo] = xor_sel<rs_mask<Y, p, bo>(), (Y != 0)>(V[p][bo], U);
+            });
+        });
+    }
+
+    template <int CTRL>
+    __device__ static uint32_t qperm(uint32_t v) {
+        return uint32_t(__builtin_amdgcn_mov_dpp(int(v), CTRL, 0xF, 0xF, false));
+    }
+    // lane-dependent register / pointer selection through bitop3 masks (a select
+    // chain would be folded into a scratch array or a kernarg load by the compiler)
+    struct Sel4 {
+        uint32_t m1, m2, m3;
+        __device__ explicit Sel4(int p)
+            : m1(p == 1 ? ~0u : 0u), m2(p == 2 ? ~0u : 0u), m3(p == 3 ? ~0u : 0u) {}
+        __device__ uint32_t pick(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) const {
+            uint32_t r = sel(m1, a1, a0);
+            r = sel(m2, a2, r);
+            return sel(m3, a3, r);
+        }
+    };
+    __device__ static uint32_t pick4(const uint32_t (&V)[Q][8], const Sel4 &s, int w) {
+        return s.pick(V[0][w], V[1][w], V[2][w], V[3][w]);
+    }
+    __device__ static uint8_t *par_of(const BsArgs &a, const Sel4 &s) {
+        uint64_t p0 = uint64_t(a.par[0]), p1 = uint64_t(a.par[1]), p2 = uint64_t(a.par[2]), p3 = uint64_t(a.par[3]);
+        const uint32_t lo = s.pick(uint32_t(p0), uint32_t(p1), uint32_t(p2), uint32_t(p3));
+        const uint32_t hi = s.pick(uint32_t(p0 >> 32), uint32_t(p1 >> 32), uint32_t(p2 >> 32), uint32_t(p3 >> 32));
+        return reinterpret_cast<uint8_t *>(uint64_t(lo) | (uint64_t(hi) << 32));
+    }
+    // full tile: exactly 4 asm stores; ragged last tile: masked (that tile is always
+    // the workgroup's last, so no counted wait depends on its store count)
+    __device__ static void store32(uint8_t *p, const uint32_t (&d)[8], int nv) {
+        if (nv >= 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) st8(p + 8 * i, d[2 * i], d[2 * i + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (i < nv) st8(p + 8 * i, d[2 * i], d[2 * i + 1]);
+        }
+    }
+    // PFT (transforms.rs:108-125) for parity node x = j^K at my layer z (last digit j):
+    // C[x][z] = det^-1 (V[x][z] + g V[j][z0+x]); lane j^K of the quad holds layer z0+x
+    // and sends its V[j] (= V[s^K] for sender s).
+    template <int K>
+    __device__ static void pft_out(const BsArgs &a, const uint32_t (&V)[Q][8], int j, uint64_t off, int nv) {
+        constexpr int CTRL = K == 1 ? 0xB1 : K == 2 ? 0x4E : 0x1B;  // quad lane i reads lane i^K
+        const int x = j ^ K;
+        const Sel4 sx(x);
+        uint32_t in[16], c[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            in[w] = pick4(V, sx, w);
+            in[8 + w] = qperm<CTRL>(in[w]);  // as sender: my V[me^K]; received: partner's V[j]
+        }
+        sfor<8>([&](auto bc) BS_INL {
+            c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
+        });
+        transpose8(c);
+        store32(par_of(a, sx) + off, c, nv);
+    }
+};
+
+template <int KD, int M>
+__global__ __launch_bounds__((Bs3Kernel<KD, M>::BLOCK)) void k_bs3_encode(BsArgs a) {
+    using Kn = Bs3Kernel<KD, M>;
+    constexpr int Q = Kn::Q, NSEC = Kn::NSEC;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int j = lane & 3, pg = (lane >> 2) & 1, gl = lane >> 3;  // quad = one PFT group
+    const int z = (wave * 8 + gl) * Q + j;
+    const uint32_t lds0 = lds_addr_of(smem), lds1 = lds_addr_of(smem + Kn::SLOT_BYTES);
+    const uint32_t xcd = blockIdx.x & 7u, slotid = blockIdx.x >> 3;
+    uint32_t tix = slotid;
+    if (tix >= a.tiles_per_xcd || xcd * a.tiles_per_xcd + tix >= a.ntiles) return;
+    // prologue: sections 0 and 1 of the first tile into slots 0 and 1
+    {
+        const uint64_t b0 = uint64_t(xcd * a.tiles_per_xcd + tix) * Kn::W;
+        Kn::template dma<0>(a, lds0, wave, lane, b0);
+        Kn::template dma<1>(a, lds1, wave, lane, b0);
+    }
+    uint32_t sidx = 0;  // sections consumed so far; slot = sidx & 1
+    bool first = true;
+    while (true) {
+        const uint64_t b0 = uint64_t(xcd * a.tiles_per_xcd + tix) * Kn::W;
+        const uint32_t ntix = tix + a.nslots;
+        const bool has_next = ntix < a.tiles_per_xcd && xcd * a.tiles_per_xcd + ntix < a.ntiles;
+        const uint64_t nb0 = uint64_t(xcd * a.tiles_per_xcd + ntix) * Kn::W;
+        uint32_t V[Q][8];
+        sfor<NSEC>([&](auto yc) BS_INL {
+            constexpr int Y = decltype(yc)::value;
+            const int slot = int(sidx & 1);
+            // VMEM ops issued after this section's fill may stay in flight: the fill of
+            // section Y+1, plus the previous tile's output stores if they came later.
+            int younger;
+            if constexpr (Y == 0) {
+                younger = Kn::n_dma(1, wave) + (first ? 0 : Kn::STORES_PER_TILE);
+            } else if constexpr (Y == 1) {
+                younger = (first ? 0 : Kn::STORES_PER_TILE) + (NSEC > 2 ? Kn::n_dma(2, wave) : (has_next ? Kn::n_dma(0, wave) : 0));
+            } else if constexpr (Y + 1 < NSEC) {
+                younger = Kn::n_dma(Y + 1, wave);
+            } else {
+                younger = has_next ? Kn::n_dma(0, wave) : 0;
+            }
+            wait_vm(younger);
+            lds_barrier();  // every wave's part of the fill has landed
+            uint32_t U[Q * 8];
+            Kn::template gather<Y>(smem + slot * Kn::SLOT_BYTES, z, pg, U);
+            lds_barrier();  // the slot has been read by every wave -> refill it
+            const uint32_t sl = slot ? lds1 : lds0;
+            if constexpr (Y + 2 < NSEC) {
+                Kn::template dma<Y + 2>(a, sl, wave, lane, b0);
+            } else {
+                if (has_next) Kn::template dma_sec<0>(Y + 2 - NSEC, a, sl, wave, lane, nb0);
+            }
+            Kn::template accumulate<Y>(U, V);
+            sidx++;
+        });
+        // parity y-section: PFT across the quad, bytes back, store
+        const uint64_t pos = b0 + uint64_t(32 * pg);
+        const int nv = pos >= a.sc ? 0 : ((a.sc - pos) / 8 > 4 ? 4 : int((a.sc - pos) / 8));
+        const uint64_t off = uint64_t(z) * a.sc + pos;
+        {
+            const typename Kn::Sel4 sj(j);
+            uint32_t c[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) c[w] = Kn::pick4(V, sj, w);
+            transpose8(c);
+            Kn::store32(Kn::par_of(a, sj) + off, c, nv);
+        }
+        Kn::template pft_out<1>(a, V, j, off, nv);
+        Kn::template pft_out<2>(a, V, j, off, nv);
+        Kn::template pft_out<3>(a, V, j, off, nv);
+        first = false;
+        if (!has_next) break;
+        tix = ntix;
+    }
+    wait_vm_n<0>();
 }
 
 }  // namespace bs

@@ -14,5 +14,5 @@ run sq  SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INS
 run ta  TA_TA_BUSY GRBM_GUI_ACTIVE && \
 run fetch FETCH_SIZE && \
 run write WRITE_SIZE && \
-run tcc TCC_HIT_sum TCC_MISS_sum && \
+run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum && \
 run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES

@@ -68,19 +68,23 @@ def test_bitsliced_encode_matches_oracle(oracle_mod, cfg, tile, scale):
     assert np.array_equal(got, ref), (cfg, tile, scale)
 
 
+@pytest.mark.parametrize("variant", ["bitsliced2", "bitsliced3"])
 @pytest.mark.parametrize("cfg", [(10, 4, 13), (8, 4, 11)])
-@pytest.mark.parametrize("scale", [1, 2, 3, 37, 200])
-def test_bitsliced2_encode_matches_oracle(oracle_mod, cfg, scale):
-    """LDS-DMA staged bit-sliced kernel: single/multiple tiles, ragged last tile,
+@pytest.mark.parametrize("scale", [1, 2, 3, 37, 200, 1000])
+def test_bitsliced23_encode_matches_oracle(oracle_mod, cfg, scale, variant):
+    """v3 is instantiated for (10,4,13) only.
+    LDS-DMA staged bit-sliced kernel: single/multiple tiles, ragged last tile,
     and more tiles than workgroups (persistent loop + cross-tile prefetch)."""
+    if variant == "bitsliced3" and cfg != (10, 4, 13):
+        pytest.skip("v3 only instantiated for (10,4,13)")
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     n = k * c.sub_chunk_no * 8 * scale * 4 - 11
     data = rand_bytes(scale * 13, n)
     ref = o.encode_array(data)
-    set_encode_path("bitsliced2")
+    set_encode_path(variant)
     got = c.encode_array(data)
-    assert last_encode_path().startswith("bitsliced2"), last_encode_path()
+    assert last_encode_path().startswith(variant), last_encode_path()
     assert np.array_equal(got, ref), (cfg, scale)
 
 
