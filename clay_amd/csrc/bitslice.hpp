@@ -937,3 +937,307 @@ __global__ __launch_bounds__((Bs3Kernel<KD, M>::BLOCK)) void k_bs3_encode(BsArgs
 
 }  // namespace bs
 }  // namespace clay
+
+namespace clay {
+namespace bs {
+
+// ===========================================================================
+// v4: v2's wave-private staging, with 16-byte LDS-DMA and bank-conflict-free LDS.
+//
+// v2 staged through global_load_lds_dword (4 B/lane): 32 DMA instructions per wave
+// and section kept the texture addresser busy ~65 % of the kernel, and its stage /
+// accumulator images had 2- to 8-way bank conflicts (75 % of LDS cycles).  v4:
+//  * global_load_lds_dwordx4: 1 KiB per instruction, 8 per wave and section.  The
+//    destination is lane-linear, so the stage image is permuted through the SOURCE
+//    address of each lane (16-B piece granularity).
+//  * lane -> (pg, j, line) map chosen against the ds_read_b128 lane groups
+//    (group = lane bit 5 and parity of bits 2..4; bits 0,1,3,4 free inside one):
+//    b0 = pg, b1 = j0, b3 = j1, b4 = ll0, b5 = ll1, b2 = ll2.
+//  * stage piece (line ll, node xn, column jc, piece pc = 2 pg + d) lives at
+//    row (xn, ll >> 1, d), slot pg + 2 ((xn + jc) & 3) + 8 (ll & 1): both a lane's own
+//    value (ll, x, j) and its companion (ll, j, x) reads hit 16 distinct slots.
+//  * accumulator (p, z, pg, h) slot XOR-swizzled by a GF(2)-linear hash of z >> 2
+//    (found by tools/acc_swizzle_exhaustive.py): every section's read-modify-write
+//    and the PFT reads (partners x = j ^ k) are conflict free.
+//  * sub-chunks are only 8-byte aligned; 16-byte DMA from 4/8-byte-aligned
+//    addresses is exact (tools/dma_align_test.hip).  The one ragged piece per row
+//    of the last tile is DMA'd from a clamped address and patched after landing.
+// Parity stores are global_store_dwordx4 from asm, so the next tile's first wait
+// can leave exactly those in flight (vmcnt(STORES)).
+// ===========================================================================
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void dma16(uint32_t lds_addr, const uint8_t *sbase, uint32_t voff) {
+    unsigned keep;  // M0 is compiler-reserved: save / restore it in the same statement
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(lds_addr), "v"(voff), "s"(sbase)
+                 : "memory");
+}
+__device__ __forceinline__ void st16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const u32x4 v = {a, b, c, d};
+    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int KD, int M>
+struct Bs4Kernel {
+    using S = Shape<KD, M>;
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
+    static_assert(Q == 4 && T == 4, "v4 lane map and swizzles are derived for q = 4, t = 4");
+    static constexpr int PG = 2, W = 64, LPW = 8;        // 2 lanes x 32 positions; 8 lines per wave
+    static constexpr int LINES = ALPHA / Q, WAVES = LINES / LPW, BLOCK = 64 * WAVES;
+    static_assert(BLOCK <= 1024 && LINES % LPW == 0, "shape");
+    static constexpr int ACC_P = ALPHA * PG * 32;        // bytes per parity row of the accumulator
+    static constexpr int ACC_BYTES = Q * ACC_P;
+    static constexpr int STAGE_BYTES = LPW * Q * Q * W;  // per wave
+    static constexpr int LDS_BYTES = ACC_BYTES + WAVES * STAGE_BYTES;
+    static constexpr int NDMA = STAGE_BYTES / 1024;
+    static constexpr int STORES = Q * 2;                 // dwordx4 stores per lane per full tile
+
+    template <int Y>
+    static constexpr int wy() { int w = 1; for (int i = 0; i < T - 1 - Y; i++) w *= Q; return w; }
+    // first layer of line `line` in section Y (digit Y = 0)
+    template <int Y>
+    __device__ static int zl(int line) { return (line / wy<Y>()) * wy<Y>() * Q + line % wy<Y>(); }
+
+    __device__ static int lane_pg(int lane) { return lane & 1; }
+    __device__ static int lane_j(int lane) { return ((lane >> 1) & 1) | ((lane >> 2) & 2); }
+    __device__ static int lane_ll(int lane) { return ((lane >> 4) & 3) | (lane & 4); }
+
+    __device__ static uint32_t acc_off(int z, int pg, int h) {
+        const int zh = z >> 2;
+        const int f = (__builtin_popcount(zh & 0x15) & 1) | ((zh & 1) ? 0xC : 0);
+        return uint32_t(zh * 256 + ((((z & 3) << 2) | (pg << 1) | h) ^ f) * 16);
+    }
+
+    // Per-lane DMA source for instruction i of section Y.  Returns false when the
+    // instruction's node is shortened (never staged).  `pos` is clamped for the
+    // ragged last tile; *partial reports a piece with only 8 valid bytes.
+    template <int Y>
+    __device__ static uint32_t dma_src(int i, int wave, int lane, uint32_t b0, uint32_t sc, uint32_t *ppos) {
+        const int s = lane & 15, r = lane >> 4;
+        const int pg = s & 1, d = r & 1;
+        const int xn = i >> 1;
+        const int ll = (s >> 3) | ((((i & 1) << 1) | (r >> 1)) << 1);
+        const int jc = (((s >> 1) & 3) - xn) & 3;
+        *ppos = b0 + uint32_t(2 * pg + d) * 16u;
+        return uint32_t(zl<Y>(wave * LPW + ll) + jc * wy<Y>()) * sc;
+    }
+
+    template <int Y>
+    __device__ static void dma(const BsArgs &a, uint32_t stage_lds, int wave, int lane, uint32_t b0) {
+        const uint32_t sc = uint32_t(a.sc);
+#pragma unroll
+        for (int i = 0; i < NDMA; i++) {
+            const int node = Y * Q + (i >> 1);
+            if (node >= KD) continue;  // shortened node: known zero, never read
+            uint32_t pos;
+            const uint32_t row = dma_src<Y>(i, wave, lane, b0, sc, &pos);
+            if (pos + 16u > sc) pos = sc - 16u;  // ragged: any valid bytes, patched after landing
+            dma16(stage_lds + uint32_t(i) * 1024u, a.data[node], row + pos);
+        }
+    }
+
+    // ragged last tile: rewrite the pieces whose DMA source was clamped
+    template <int Y>
+    __device__ static void patch(const BsArgs &a, uint8_t *stage, int wave, int lane, uint32_t b0) {
+        const uint32_t sc = uint32_t(a.sc);
+#pragma unroll
+        for (int i = 0; i < NDMA; i++) {
+            const int node = Y * Q + (i >> 1);
+            if (node >= KD) continue;
+            uint32_t pos;
+            const uint32_t row = dma_src<Y>(i, wave, lane, b0, sc, &pos);
+            if (pos < sc && pos + 16u > sc) {  // 8 valid bytes (sc is a multiple of 8)
+                const uint2 v = *reinterpret_cast<const uint2 *>(a.data[node] + row + pos);
+                *reinterpret_cast<uint4 *>(stage + i * 1024 + lane * 16) = make_uint4(v.x, v.y, 0u, 0u);
+            }
+        }
+    }
+
+    __device__ static void read32(const uint8_t *p, uint32_t (&d)[8]) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(p), v1 = *reinterpret_cast<const uint4 *>(p + 256);
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+
+    template <int Y, int P, int BO>
+    static constexpr uint64_t rs_mask() {
+        uint64_t m = 0;
+        for (int x = 0; x < Q; x++) m |= plane_mask(S::RS.g[P][Y * Q + x], BO, 8 * x);
+        return m;
+    }
+    template <int BO>
+    static constexpr uint64_t pft_mask() {
+        return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
+    }
+
+    template <int Y>
+    __device__ static void section(const BsArgs &a, uint8_t *acc, uint8_t *stage, int wave, int lane,
+                                   uint32_t b0, uint32_t nb0, bool has_next, bool first, bool ragged) {
+        constexpr int WY = wy<Y>();
+        const int pg = lane_pg(lane), j = lane_j(lane), ll = lane_ll(lane);
+        const int zj = zl<Y>(wave * LPW + ll) + j * WY;
+        const bool creal = (Y * Q + j) < KD;
+        if constexpr (Y == 0) {
+            if (first) wait_vm_n<0>();
+            else wait_vm_n<STORES>();  // previous tile's parity stores may stay in flight
+        } else {
+            wait_vm_n<0>();
+        }
+        if (ragged) patch<Y>(a, stage, wave, lane, b0);
+        const int lbase = (ll >> 1) * 512 + (pg + 8 * (ll & 1)) * 16;
+        uint32_t U[Q * 8];
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            const int sw = ((x + j) & 3) * 32;
+            uint32_t o[8], c[8];
+            if constexpr (Y * Q + x < KD) {
+                read32(stage + x * 2048 + lbase + sw, o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) o[w] = 0;
+            }
+            read32(stage + j * 2048 + lbase + sw, c);
+            const uint32_t keep = (creal && x != j) ? 0xffffffffu : 0u;
+            const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+#pragma unroll
+            for (int w = 0; w < 8; w++) U[x * 8 + w] = xor_xtime4_masked(o[w], c[w], ks, kr);
+        });
+        // the wave's stage is in registers -> refill it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (Y + 1 < T - 1) {
+            dma<Y + 1>(a, lds_addr_of(stage), wave, lane, b0);
+        } else {
+            if (has_next) dma<0>(a, lds_addr_of(stage), wave, lane, nb0);
+        }
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t t[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) t[w] = U[x * 8 + w];
+            transpose8(t);
+#pragma unroll
+            for (int w = 0; w < 8; w++) U[x * 8 + w] = t[w];
+        });
+        const uint32_t a0 = acc_off(zj, pg, 0), a1 = acc_off(zj, pg, 1);
+        sfor<Q>([&](auto pc) BS_INL {
+            constexpr int p = decltype(pc)::value;
+            uint4 *l0 = reinterpret_cast<uint4 *>(acc + p * ACC_P + a0);
+            uint4 *l1 = reinterpret_cast<uint4 *>(acc + p * ACC_P + a1);
+            uint32_t V[8];
+            if constexpr (Y == 0) {
+                sfor<8>([&](auto bc) BS_INL {
+                    V[decltype(bc)::value] = xor_sel<rs_mask<Y, p, decltype(bc)::value>(), false>(0u, U);
+                });
+            } else {
+                const uint4 v0 = *l0, v1 = *l1;
+                V[0] = v0.x; V[1] = v0.y; V[2] = v0.z; V[3] = v0.w;
+                V[4] = v1.x; V[5] = v1.y; V[6] = v1.z; V[7] = v1.w;
+                sfor<8>([&](auto bc) BS_INL {
+                    V[decltype(bc)::value] = xor_sel<rs_mask<Y, p, decltype(bc)::value>(), true>(V[decltype(bc)::value], U);
+                });
+            }
+            *l0 = make_uint4(V[0], V[1], V[2], V[3]);
+            *l1 = make_uint4(V[4], V[5], V[6], V[7]);
+        });
+    }
+
+    // lane-dependent parity node: uniform pointer loads + selects (no divergent kernarg load)
+    // (each pointer is pinned in SGPRs first; otherwise the compiler folds the selects
+    // back into a per-lane global_load whose vmcnt(0) would drain the DMA prefetch)
+    __device__ static uint8_t *par_of(const BsArgs &a, int x) {
+        uint64_t r = reinterpret_cast<uint64_t>(a.par[0]);
+        asm volatile("" : "+s"(r));
+#pragma unroll
+        for (int i = 1; i < Q; i++) {
+            uint64_t pi = reinterpret_cast<uint64_t>(a.par[i]);
+            asm volatile("" : "+s"(pi));
+            r = (x == i) ? pi : r;
+        }
+        return reinterpret_cast<uint8_t *>(r);
+    }
+
+    __device__ static void read_acc(const uint8_t *acc, int p, int z, int pg, uint32_t *v) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(acc + p * ACC_P + acc_off(z, pg, 0));
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(acc + p * ACC_P + acc_off(z, pg, 1));
+        v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+        v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    }
+
+    __device__ static void store32(uint8_t *p, const uint32_t (&d)[8], bool full, int nv) {
+        if (full) {
+            st16(p, d[0], d[1], d[2], d[3]);
+            st16(p + 16, d[4], d[5], d[6], d[7]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
+        }
+    }
+
+    // PFT of the parity y-section (digit t-1, weight 1) for this wave's groups + store.
+    __device__ static void finish(const BsArgs &a, const uint8_t *acc, int wave, int lane, uint32_t b0, bool ragged) {
+        const int pg = lane_pg(lane), j = lane_j(lane), gl = lane_ll(lane);
+        const int z0 = (wave * LPW + gl) * Q;
+        const uint32_t sc = uint32_t(a.sc);
+        const uint32_t pos = b0 + uint32_t(32 * pg);
+        const int nv = pos >= sc ? 0 : ((sc - pos) / 8 > 4 ? 4 : int((sc - pos) / 8));
+        const bool full = !ragged;
+        const uint32_t off = uint32_t(z0 + j) * sc + pos;
+        {
+            uint32_t v[8];
+            read_acc(acc, j, z0 + j, pg, v);
+            transpose8(v);
+            store32(par_of(a, j) + off, v, full, nv);
+        }
+#pragma unroll
+        for (int k = 1; k < Q; k++) {
+            const int x = j ^ k;
+            uint32_t in[16], c[8];
+            read_acc(acc, x, z0 + j, pg, in);
+            read_acc(acc, j, z0 + x, pg, in + 8);
+            sfor<8>([&](auto bc) BS_INL {
+                c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
+            });
+            transpose8(c);
+            store32(par_of(a, x) + off, c, full, nv);
+        }
+    }
+};
+
+template <int KD, int M>
+__global__ __launch_bounds__((Bs4Kernel<KD, M>::BLOCK)) void k_bs4_encode(BsArgs a) {
+    using Kn = Bs4Kernel<KD, M>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *acc = smem;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    uint8_t *stage = smem + Kn::ACC_BYTES + wave * Kn::STAGE_BYTES;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    uint32_t tix = slot;
+    uint32_t tile = xcd * a.tiles_per_xcd + tix;
+    if (tix >= a.tiles_per_xcd || tile >= a.ntiles) return;
+    Kn::template dma<0>(a, lds_addr_of(stage), wave, lane, tile * uint32_t(Kn::W));
+    bool first = true;
+    while (true) {
+        const uint32_t b0 = tile * uint32_t(Kn::W);
+        const bool ragged = uint64_t(b0) + Kn::W > a.sc;
+        const uint32_t ntix = tix + a.nslots, ntile = xcd * a.tiles_per_xcd + ntix;
+        const bool has_next = ntix < a.tiles_per_xcd && ntile < a.ntiles;
+        const uint32_t nb0 = ntile * uint32_t(Kn::W);
+        sfor<Kn::T - 1>([&](auto yc) BS_INL {
+            Kn::template section<decltype(yc)::value>(a, acc, stage, wave, lane, b0, nb0, has_next, first, ragged);
+            lds_barrier();
+        });
+        Kn::finish(a, acc, wave, lane, b0, ragged);
+        lds_barrier();
+        if (!has_next) break;
+        first = false;
+        tix = ntix;
+        tile = ntile;
+    }
+    wait_vm0();
+}
+
+}  // namespace bs
+}  // namespace clay
