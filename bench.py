@@ -45,7 +45,8 @@ def parse():
                     help="bound on the CPU-baseline sample (0 disables)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
-    ap.add_argument("--path", default="auto", choices=["auto", "fused", "staged"])
+    ap.add_argument("--path", default="auto",
+                    choices=["auto", "fused", "staged", "bitsliced", "bitsliced2", "bitsliced3", "bitsliced4", "bitsliced5", "bitsliced6"])
     return ap.parse_args()
 
 

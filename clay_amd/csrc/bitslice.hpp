@@ -1241,3 +1241,373 @@ __global__ __launch_bounds__((Bs4Kernel<KD, M>::BLOCK)) void k_bs4_encode(BsArgs
 
 }  // namespace bs
 }  // namespace clay
+
+namespace clay {
+namespace bs {
+
+// ===========================================================================
+// v5: layer-per-lane register accumulators + a ring of node slots (16-byte DMA).
+//
+// v4 keeps the parity accumulators in LDS (64 KiB) and one 8 KiB stage per wave,
+// so only one section (64 KiB per CU) is ever in flight and each section's wait
+// is one section of compute after its issue.  v5 frees the LDS for data:
+//  * lane (layer z, half pg) owns acc[p][plane] (32 VGPRs) for the whole tile --
+//    every (line, column) step of the reference's per-layer loop is one (layer,
+//    section) pair of this lane, so no accumulator ever moves;
+//  * LDS = 10 node slots of alpha x 64 B = 160 KiB; data node n of a tile always
+//    lives in slot n.  A section's slots are refilled with the NEXT tile's
+//    section as soon as every wave has read them (right after the next section's
+//    barrier), so each section's DMA is issued two sections before it is read;
+//  * slot image: 16-byte piece (layer, pg, d) at bank slot B.(layer|pg<<8|d<<9)
+//    ^ H.node, rows completing a GF(2) bijection (tools/v5_layout_search.py):
+//    own reads (node x, layer z) and companion reads (node z_Y, layer z with
+//    digit Y := x) of every section are bank-conflict free on ds_read_b128;
+//  * lane bits 0-1 = digit t-1 of z, so the PFT partners of the parity
+//    y-section are a lane quad: exchange via DPP quad_perm, no LDS.
+// One barrier per section; waits are counted vmcnt (DMA and the asm parity
+// stores are the only VMEM ops in flight).
+// ===========================================================================
+namespace v5 {
+constexpr uint32_t BM[4] = {0x297, 0x134, 0x328, 0x62};  // bank bit o = <v, BM[o]> ^ <node, HM[o]>
+constexpr uint32_t HM[4] = {0, 0, 2, 0};
+constexpr int par10(uint32_t v) { int p = 0; for (; v; v &= v - 1) p ^= 1; return p; }
+struct Lin {
+    uint16_t fwd[10];  // column i: piece index (row << 4 | bank) of unit vector e_i
+    uint16_t inv[10];  // column i: v of piece-index unit vector e_i
+};
+constexpr Lin make_lin() {
+    Lin L{};
+    // rows 4..9 of M: unit vectors completing the row space of BM
+    uint32_t rows[10] = {BM[0], BM[1], BM[2], BM[3], 0, 0, 0, 0, 0, 0};
+    int nr = 4;
+    for (int b = 0; b < 10 && nr < 10; b++) {
+        // is e_b independent of rows[0..nr)?  reduce by Gaussian elimination
+        uint32_t basis[10] = {};
+        int piv[10] = {};
+        int nb = 0;
+        for (int r = 0; r < nr; r++) {
+            uint32_t v = rows[r];
+            for (int i = 0; i < nb; i++)
+                if ((v >> piv[i]) & 1) v ^= basis[i];
+            if (v) { int p = 0; while (!((v >> p) & 1)) p++; basis[nb] = v; piv[nb] = p; nb++; }
+        }
+        uint32_t v = 1u << b;
+        for (int i = 0; i < nb; i++)
+            if ((v >> piv[i]) & 1) v ^= basis[i];
+        if (v) rows[nr++] = 1u << b;
+    }
+    // piece index bit layout: bank bits 0..3 = rows 0..3, row bits 4..9 = rows 4..9
+    for (int i = 0; i < 10; i++) {
+        uint16_t p = 0;
+        for (int r = 0; r < 10; r++)
+            if ((rows[r] >> i) & 1) p |= uint16_t(1u << r);
+        L.fwd[i] = p;
+    }
+    // invert the 10x10 matrix whose column i is fwd[i]
+    uint32_t a[10] = {}, inv[10] = {};
+    for (int r = 0; r < 10; r++) {
+        for (int i = 0; i < 10; i++)
+            if ((L.fwd[i] >> r) & 1) a[r] |= 1u << i;
+        inv[r] = 1u << r;
+    }
+    for (int c = 0; c < 10; c++) {
+        int p = c;
+        while (!((a[p] >> c) & 1)) p++;
+        uint32_t t = a[p]; a[p] = a[c]; a[c] = t;
+        t = inv[p]; inv[p] = inv[c]; inv[c] = t;
+        for (int r = 0; r < 10; r++)
+            if (r != c && ((a[r] >> c) & 1)) { a[r] ^= a[c]; inv[r] ^= inv[c]; }
+    }
+    // inv[r] is row r of M^-1: v bit r = <p, inv[r]>; store columns
+    for (int i = 0; i < 10; i++) {
+        uint16_t col = 0;
+        for (int r = 0; r < 10; r++)
+            if ((inv[r] >> i) & 1) col |= uint16_t(1u << r);
+        L.inv[i] = col;
+    }
+    return L;
+}
+constexpr Lin LIN = make_lin();
+constexpr uint32_t fwd_c(uint32_t v) { uint32_t p = 0; for (int i = 0; i < 10; i++) if ((v >> i) & 1) p ^= LIN.fwd[i]; return p; }
+constexpr uint32_t inv_c(uint32_t p) { uint32_t v = 0; for (int i = 0; i < 10; i++) if ((p >> i) & 1) v ^= LIN.inv[i]; return v; }
+constexpr uint32_t hbank(int node) {
+    uint32_t b = 0;
+    for (int o = 0; o < 4; o++) b |= uint32_t(par10(uint32_t(node) & HM[o])) << o;
+    return b;
+}
+static_assert(inv_c(fwd_c(0x2A5)) == 0x2A5 && inv_c(fwd_c(0x13F)) == 0x13F, "layout bijection");
+__device__ __forceinline__ uint32_t fwd_d(uint32_t v) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) p ^= ((v >> i) & 1) ? uint32_t(LIN.fwd[i]) : 0u;
+    return p;
+}
+__device__ __forceinline__ uint32_t inv_d(uint32_t p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) v ^= ((p >> i) & 1) ? uint32_t(LIN.inv[i]) : 0u;
+    return v;
+}
+}  // namespace v5
+
+template <int KD, int M>
+struct Bs5Kernel {
+    using S = Shape<KD, M>;
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
+    static_assert(KD == 10 && M == 4 && Q == 4 && T == 4 && ALPHA == 256,
+                  "v5 layout and slot ring are derived for (10,4,13)");
+    static constexpr int PG = 2, W = 64, BLOCK = ALPHA * PG, WAVES = BLOCK / 64;
+    static constexpr int SLOT = ALPHA * W;                 // 16 KiB per data node
+    static constexpr int LDS_BYTES = KD * SLOT;            // 160 KiB
+    static constexpr int NDMA = SLOT / 1024 / WAVES;       // per wave per node: 2
+    static constexpr int STORES = Q * 2;
+
+    template <int Y>
+    static constexpr int nreal() { int n = 0; for (int x = 0; x < Q; x++) n += (Y * Q + x < KD); return n; }
+    template <int Y>
+    static constexpr int ndma() { return nreal<Y>() * NDMA; }
+    static constexpr int dshift(int y) { return 2 * (T - 1 - y); }
+
+    // byte offset inside the tile of piece v = layer | pg << 8 | d << 9
+    __device__ static uint32_t piece_off(uint32_t v) { return ((v >> 8) & 1u) * 32u + (v >> 9) * 16u; }
+
+    __device__ static int lane_z(int l) { return ((l >> 3) << 2) | (l & 3); }
+    __device__ static int lane_pg(int l) { return (l >> 2) & 1; }
+
+    // DMA of data y-section Y of the tile at b0 into the node slots.  Wave w
+    // writes pieces [1024 (NDMA w + i), +1024) of each node slot.
+    template <int Y>
+    __device__ static void dma(const BsArgs &a, uint32_t lds0, int wave, int lane, uint32_t b0) {
+        const uint32_t sc = uint32_t(a.sc);
+        uint32_t vl = v5::inv_d(uint32_t(lane));
+        asm volatile("" : "+v"(vl));  // recompute per call: keeps ~20 offsets out of the live set
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            if constexpr (node < KD) {
+#pragma unroll
+                for (int i = 0; i < NDMA; i++) {
+                    const uint32_t blk = uint32_t(wave * NDMA + i);  // 1 KiB block = piece bits 6..9
+                    const uint32_t v = vl ^ v5::inv_d((blk << 6) ^ v5::hbank(node));
+                    uint32_t pos = b0 + piece_off(v);
+                    if (pos + 16u > sc) pos = sc - 16u;  // ragged: patched after landing
+                    dma16(lds0 + uint32_t(node * SLOT) + blk * 1024u, a.data[node], (v & 255u) * sc + pos);
+                }
+            }
+        });
+    }
+    template <int Y>
+    __device__ static void patch(const BsArgs &a, uint8_t *lds, int wave, int lane, uint32_t b0) {
+        const uint32_t sc = uint32_t(a.sc);
+        uint32_t vl = v5::inv_d(uint32_t(lane));
+        asm volatile("" : "+v"(vl));  // recompute per call: keeps ~20 offsets out of the live set
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            if constexpr (node < KD) {
+#pragma unroll
+                for (int i = 0; i < NDMA; i++) {
+                    const uint32_t blk = uint32_t(wave * NDMA + i);
+                    const uint32_t v = vl ^ v5::inv_d((blk << 6) ^ v5::hbank(node));
+                    const uint32_t pos = b0 + piece_off(v);
+                    if (pos < sc && pos + 16u > sc) {
+                        const uint2 g = *reinterpret_cast<const uint2 *>(a.data[node] + (v & 255u) * sc + pos);
+                        *reinterpret_cast<uint4 *>(lds + node * SLOT + blk * 1024 + lane * 16) =
+                            make_uint4(g.x, g.y, 0u, 0u);
+                    }
+                }
+            }
+        });
+    }
+
+    __device__ static void read32(const uint8_t *lds, uint32_t off0, uint32_t off1, uint32_t (&d)[8]) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(lds + off0);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(lds + off1);
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+
+    template <int Y, int P, int BO>
+    static constexpr uint64_t rs_mask() {
+        uint64_t m = 0;
+        for (int x = 0; x < Q; x++) m |= plane_mask(S::RS.g[P][Y * Q + x], BO, 8 * x);
+        return m;
+    }
+    template <int BO>
+    static constexpr uint64_t pft_mask() {
+        return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
+    }
+
+    // Section Y: stage -> U (PRT) -> bit planes -> acc += RS.
+    template <int Y>
+    __device__ static void section(const uint8_t *lds, int z, int pg, uint32_t (&acc)[Q * 8]) {
+        constexpr int sh = dshift(Y);
+        const int zy = (z >> sh) & 3;
+        const bool creal = (Y * Q + zy) < KD;
+        // piece index of (layer, pg, d=0) with digit Y cleared, and of the own layer
+        const uint32_t fown = v5::fwd_d(uint32_t(z) | uint32_t(pg << 8));
+        const uint32_t fcl = v5::fwd_d(uint32_t(z & ~(3 << sh)) | uint32_t(pg << 8));
+        const int cnode = Y * Q + (creal ? zy : 0);
+        const uint32_t cbase = uint32_t(cnode * SLOT);
+        // node-dependent bank XOR of the companion node (lane-dependent node)
+        uint32_t hb = 0;
+#pragma unroll
+        for (int o = 0; o < 4; o++) hb |= uint32_t(v5::par10(uint32_t(cnode) & v5::HM[o]) & 1) << o;
+        constexpr uint32_t FD = v5::fwd_c(1u << 9);
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            uint32_t o[8], c[8];
+            if constexpr (node < KD) {
+                constexpr uint32_t hn = v5::hbank(node);
+                read32(lds, uint32_t(node * SLOT) + 16u * (fown ^ hn), uint32_t(node * SLOT) + 16u * (fown ^ hn ^ FD), o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) o[w] = 0;
+            }
+            constexpr uint32_t FX = v5::fwd_c(uint32_t(x) << sh);
+            const uint32_t cp = fcl ^ FX ^ hb;
+            if (creal) {
+                read32(lds, cbase + 16u * cp, cbase + 16u * (cp ^ FD), c);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) c[w] = 0;
+            }
+            const uint32_t keep = (creal && x != zy) ? 0xffffffffu : 0u;
+            const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+            uint32_t u[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], c[w], ks, kr);
+            transpose8(u);
+            // fold this node's U into every parity accumulator: acc[p] ^= g[p][Yq+x] * U[x]
+            sfor<Q>([&](auto pc) BS_INL {
+                constexpr int p = decltype(pc)::value;
+                sfor<8>([&](auto bc) BS_INL {
+                    constexpr int bo = decltype(bc)::value;
+                    constexpr uint64_t mk = plane_mask(S::RS.g[p][Y * Q + x], bo, 0);
+                    acc[p * 8 + bo] = xor_sel<mk, (Y > 0 || x > 0)>(acc[p * 8 + bo], u);
+                });
+            });
+        });
+    }
+
+    __device__ static uint8_t *par_of(const BsArgs &a, int x) {
+        uint64_t r = reinterpret_cast<uint64_t>(a.par[0]);
+        asm volatile("" : "+s"(r));
+#pragma unroll
+        for (int i = 1; i < Q; i++) {
+            uint64_t pi = reinterpret_cast<uint64_t>(a.par[i]);
+            asm volatile("" : "+s"(pi));
+            r = (x == i) ? pi : r;
+        }
+        return reinterpret_cast<uint8_t *>(r);
+    }
+
+    template <int K>
+    __device__ static uint32_t qxor(uint32_t v) {
+        constexpr int ctrl = K == 1 ? 0xB1 : K == 2 ? 0x4E : 0x1B;  // quad_perm lane ^ K
+        return uint32_t(__builtin_amdgcn_mov_dpp(int(v), ctrl, 0xF, 0xF, true));
+    }
+
+    // PFT of the parity y-section (digit t-1 = lane bits 0-1) and the parity stores.
+    __device__ static void finish(const BsArgs &a, const uint32_t (&acc)[Q * 8], int z, int pg, uint32_t b0,
+                                  bool ragged) {
+        const uint32_t sc = uint32_t(a.sc);
+        const int d3 = z & 3;
+        const uint32_t m0 = (d3 & 1) ? 0xffffffffu : 0u, m1 = (d3 & 2) ? 0xffffffffu : 0u;
+        const uint32_t pos = b0 + uint32_t(32 * pg);
+        const int nv = pos >= sc ? 0 : ((sc - pos) / 8 > 4 ? 4 : int((sc - pos) / 8));
+        const uint32_t off = uint32_t(z) * sc + pos;
+        sfor<Q>([&](auto kc) BS_INL {
+            constexpr int k = decltype(kc)::value;
+            // s = acc[d3 ^ k] (8 planes): select on the two index bits, flipped by k
+            uint32_t s[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+                const uint32_t a0 = acc[(0 ^ k) * 8 + w], a1 = acc[(1 ^ k) * 8 + w];
+                const uint32_t a2 = acc[(2 ^ k) * 8 + w], a3 = acc[(3 ^ k) * 8 + w];
+                s[w] = sel(m1, sel(m0, a3, a2), sel(m0, a1, a0));
+            }
+            uint32_t c[8];
+            if constexpr (k == 0) {
+#pragma unroll
+                for (int w = 0; w < 8; w++) c[w] = s[w];
+            } else {
+                uint32_t in[16];
+#pragma unroll
+                for (int w = 0; w < 8; w++) { in[w] = s[w]; in[8 + w] = qxor<k>(s[w]); }
+                sfor<8>([&](auto bc) BS_INL {
+                    c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
+                });
+            }
+            transpose8(c);
+            uint8_t *p = par_of(a, d3 ^ k) + off;
+            if (!ragged) {
+                st16(p, c[0], c[1], c[2], c[3]);
+                st16(p + 16, c[4], c[5], c[6], c[7]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(c[2 * i], c[2 * i + 1]);
+            }
+        });
+    }
+};
+
+template <int KD, int M>
+__global__ __launch_bounds__((Bs5Kernel<KD, M>::BLOCK)) void k_bs5_encode(BsArgs a) {
+    using Kn = Bs5Kernel<KD, M>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int z = Kn::lane_z(int(threadIdx.x)), pg = Kn::lane_pg(int(threadIdx.x));
+    const uint32_t lds0 = lds_addr_of(smem);
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    uint32_t tix = slot;
+    uint32_t tile = xcd * a.tiles_per_xcd + tix;
+    if (tix >= a.tiles_per_xcd || tile >= a.ntiles) return;
+    {
+        const uint32_t b0 = tile * uint32_t(Kn::W);
+        Kn::template dma<0>(a, lds0, wave, lane, b0);
+        Kn::template dma<1>(a, lds0, wave, lane, b0);
+        Kn::template dma<2>(a, lds0, wave, lane, b0);
+    }
+    bool first = true;
+    uint32_t acc[Kn::Q * 8];
+    while (true) {
+        const uint32_t b0 = tile * uint32_t(Kn::W);
+        const bool ragged = uint64_t(b0) + Kn::W > a.sc;
+        const uint32_t ntix = tix + a.nslots, ntile = xcd * a.tiles_per_xcd + ntix;
+        const bool has_next = ntix < a.tiles_per_xcd && ntile < a.ntiles;
+        const uint32_t nb0 = ntile * uint32_t(Kn::W);
+        // section 0: younger than its DMA: S1 (+ S2 on the first tile) or S1 + last stores
+        if (first) wait_vm_n<Kn::template ndma<1>() + Kn::template ndma<2>()>();
+        else wait_vm_n<Kn::template ndma<1>() + Kn::STORES>();
+        if (ragged) Kn::template patch<0>(a, smem, wave, lane, b0);
+        lds_barrier();
+        if (!first) Kn::template dma<2>(a, lds0, wave, lane, b0);  // S2 slots <- this tile's S2
+        Kn::template section<0>(smem, z, pg, acc);
+        // section 1
+        if (first) wait_vm_n<Kn::template ndma<2>()>();
+        else wait_vm_n<Kn::STORES + Kn::template ndma<2>()>();
+        if (ragged) Kn::template patch<1>(a, smem, wave, lane, b0);
+        lds_barrier();
+        if (has_next) Kn::template dma<0>(a, lds0, wave, lane, nb0);  // S0 slots <- next tile
+        Kn::template section<1>(smem, z, pg, acc);
+        // section 2
+        if (has_next) wait_vm_n<Kn::template ndma<0>()>();
+        else wait_vm_n<0>();
+        if (ragged) Kn::template patch<2>(a, smem, wave, lane, b0);
+        lds_barrier();
+        if (has_next) Kn::template dma<1>(a, lds0, wave, lane, nb0);  // S1 slots <- next tile
+        Kn::template section<2>(smem, z, pg, acc);
+        Kn::finish(a, acc, z, pg, b0, ragged);
+        if (!has_next) break;
+        first = false;
+        tix = ntix;
+        tile = ntile;
+    }
+    wait_vm0();
+}
+
+}  // namespace bs
+}  // namespace clay

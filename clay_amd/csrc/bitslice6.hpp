@@ -1,0 +1,421 @@
+// bitslice6.hpp -- v6 bit-sliced encode for (10,4,13): 128-byte runs per sub-chunk row.
+//
+// Why: the v4 kernel (64-byte tiles) runs at the ceiling of its own access pattern --
+// tools/dmabench2 shows 64-byte runs per sub-chunk row cap the LDS-DMA sweep at ~3.8 TB/s
+// and 128-byte runs reach ~4.6 TB/s (reads + parity stores, no math).  v4's accumulators
+// (64 KiB LDS per 64-byte tile) leave no room to double the tile, so v6 re-partitions:
+//
+//  * lane = (column c = (d0,d1,d2) of the layer digits, part = 32-byte quarter of the
+//    128-byte tile); it owns the four layers z = 4c + g, g = d3 = the digit of the
+//    parity y-section.  Every PFT partner pair (x, z) <-> (d3(z), z with d3 := x) then
+//    lives in ONE lane: the PFT needs no exchange at all.
+//  * the lines of the data y-sections 0..2 never change d3, so a tile is processed as
+//    12 steps (group g, section Y), each reading one "slot": 4 nodes x 64 layers x 128 B
+//    = 32 KiB.  Slots stream through a 5-deep LDS ring (160 KiB) by 16-byte LDS-DMA,
+//    issued 4 steps ahead; one barrier per step; counted vmcnt waits.
+//  * accumulators: the current group's 4 parity x 8 planes (32 VGPRs) plus the U values
+//    later groups' PFT pairs need (at most 6 x 8 VGPRs), all in registers.  When group g
+//    finishes, its red vertex and its PFT pairs with groups h < g are written out.
+//  * slot image: 16-byte piece (c, part, d) of node x at bank slot B.(c|part<<6|d<<8)
+//    ^ H.x (tools/v6_layout_search.py): own and companion ds_read_b128 of every section
+//    are bank-conflict free.
+#pragma once
+
+#include "bitslice.hpp"
+
+namespace clay {
+namespace bs {
+
+// GF(2)-linear piece map: NB input bits v -> piece index p = (row << 4) | bank, with
+// bank bit o = <v, BM[o]> and rows completing the bijection with unit vectors.
+template <int NB>
+struct GfLin {
+    uint16_t fwd[NB];  // column i: p of unit vector e_i
+    uint16_t inv[NB];  // column i: v of unit vector e_i in piece-index space
+};
+template <int NB>
+constexpr GfLin<NB> make_gflin(const uint32_t (&bm)[4]) {
+    GfLin<NB> L{};
+    uint32_t rows[NB] = {};
+    int nr = 0;
+    for (int o = 0; o < 4; o++) rows[nr++] = bm[o];
+    for (int b = 0; b < NB && nr < NB; b++) {
+        uint32_t basis[NB] = {};
+        int piv[NB] = {};
+        int nb = 0;
+        for (int r = 0; r < nr; r++) {
+            uint32_t v = rows[r];
+            for (int i = 0; i < nb; i++)
+                if ((v >> piv[i]) & 1) v ^= basis[i];
+            if (v) {
+                int p = 0;
+                while (!((v >> p) & 1)) p++;
+                basis[nb] = v;
+                piv[nb] = p;
+                nb++;
+            }
+        }
+        uint32_t v = 1u << b;
+        for (int i = 0; i < nb; i++)
+            if ((v >> piv[i]) & 1) v ^= basis[i];
+        if (v) rows[nr++] = 1u << b;
+    }
+    for (int i = 0; i < NB; i++) {
+        uint16_t p = 0;
+        for (int r = 0; r < NB; r++)
+            if ((rows[r] >> i) & 1) p |= uint16_t(1u << r);
+        L.fwd[i] = p;
+    }
+    uint32_t a[NB] = {}, inv[NB] = {};
+    for (int r = 0; r < NB; r++) {
+        for (int i = 0; i < NB; i++)
+            if ((L.fwd[i] >> r) & 1) a[r] |= 1u << i;
+        inv[r] = 1u << r;
+    }
+    for (int c = 0; c < NB; c++) {
+        int p = c;
+        while (!((a[p] >> c) & 1)) p++;
+        uint32_t t = a[p];
+        a[p] = a[c];
+        a[c] = t;
+        t = inv[p];
+        inv[p] = inv[c];
+        inv[c] = t;
+        for (int r = 0; r < NB; r++)
+            if (r != c && ((a[r] >> c) & 1)) {
+                a[r] ^= a[c];
+                inv[r] ^= inv[c];
+            }
+    }
+    for (int i = 0; i < NB; i++) {
+        uint16_t col = 0;
+        for (int r = 0; r < NB; r++)
+            if ((inv[r] >> i) & 1) col |= uint16_t(1u << r);
+        L.inv[i] = col;
+    }
+    return L;
+}
+
+namespace v6 {
+constexpr uint32_t BM[4] = {0xf3, 0x85, 0x17a, 0x1e5};  // over v = c | part << 6 | d << 8
+constexpr uint32_t HM[4] = {0, 0, 3, 2};                // over the slot-local node x
+constexpr GfLin<9> LIN = make_gflin<9>(BM);
+constexpr int par32(uint32_t v) {
+    int p = 0;
+    for (; v; v &= v - 1) p ^= 1;
+    return p;
+}
+constexpr uint32_t fwd_c(uint32_t v) {
+    uint32_t p = 0;
+    for (int i = 0; i < 9; i++)
+        if ((v >> i) & 1) p ^= LIN.fwd[i];
+    return p;
+}
+constexpr uint32_t inv_c(uint32_t p) {
+    uint32_t v = 0;
+    for (int i = 0; i < 9; i++)
+        if ((p >> i) & 1) v ^= LIN.inv[i];
+    return v;
+}
+constexpr uint32_t hbank(int x) {
+    uint32_t b = 0;
+    for (int o = 0; o < 4; o++) b |= uint32_t(par32(uint32_t(x) & HM[o])) << o;
+    return b;
+}
+static_assert(inv_c(fwd_c(0x1A5)) == 0x1A5 && inv_c(fwd_c(0x0FF)) == 0x0FF, "v6 layout bijection");
+static_assert((fwd_c(0x1FF) & 15) == ((par32(0x1FF & BM[0])) | (par32(0x1FF & BM[1]) << 1) |
+                                      (par32(0x1FF & BM[2]) << 2) | (par32(0x1FF & BM[3]) << 3)),
+              "bank bits of the piece index");
+__device__ __forceinline__ uint32_t fwd_d(uint32_t v) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) p ^= ((v >> i) & 1) ? uint32_t(LIN.fwd[i]) : 0u;
+    return p;
+}
+__device__ __forceinline__ uint32_t inv_d(uint32_t p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) v ^= ((p >> i) & 1) ? uint32_t(LIN.inv[i]) : 0u;
+    return v;
+}
+__device__ __forceinline__ uint32_t hbank_d(uint32_t x) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int o = 0; o < 4; o++) b |= uint32_t(__builtin_popcount(x & HM[o]) & 1) << o;
+    return b;
+}
+}  // namespace v6
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field)
+__device__ __forceinline__ void wait_vm_rt(int n) {
+    switch (n < 63 ? n : 63) {
+#define CLAY_W1(k) case k: wait_vm_n<k>(); break;
+#define CLAY_W8(k) CLAY_W1(k) CLAY_W1(k + 1) CLAY_W1(k + 2) CLAY_W1(k + 3) CLAY_W1(k + 4) CLAY_W1(k + 5) CLAY_W1(k + 6) CLAY_W1(k + 7)
+        CLAY_W8(0) CLAY_W8(8) CLAY_W8(16) CLAY_W8(24) CLAY_W8(32) CLAY_W8(40) CLAY_W8(48) CLAY_W8(56)
+#undef CLAY_W8
+#undef CLAY_W1
+        default: wait_vm_n<0>(); break;
+    }
+}
+
+template <int KD, int M>
+struct Bs6Kernel {
+    using S = Shape<KD, M>;
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
+    static_assert(KD == 10 && M == 4 && Q == 4 && T == 4 && ALPHA == 256,
+                  "v6 slot layout is derived for (10,4,13)");
+    static constexpr int W = 128, PARTS = 4, COLS = ALPHA / Q, BLOCK = COLS * PARTS, WAVES = BLOCK / 64;
+    static constexpr int NODE_BYTES = COLS * W;            // 8 KiB: one node of one (Y, g) slot
+    static constexpr int SLOT = Q * NODE_BYTES;            // 32 KiB
+    static constexpr int RING = 5;
+    static constexpr int LDS_BYTES = RING * SLOT;          // 160 KiB
+    static constexpr int AHEAD = RING - 1;                 // slots in flight ahead of the read
+    static constexpr int STEPS = (T - 1) * Q;              // (section, group) steps per tile
+    static constexpr int DMA_PER_NODE = NODE_BYTES / 1024 / WAVES;  // per wave: 2
+
+    static constexpr int nreal(int y) { int n = 0; for (int x = 0; x < Q; x++) n += (y * Q + x < KD); return n; }
+    static constexpr int ndma(int y) { return nreal(y) * DMA_PER_NODE; }
+    static constexpr int stores(int g) { return (1 + 2 * g) * 2; }  // dwordx4 per lane at group end
+    static constexpr int dshift(int y) { return 2 * (T - 2 - y); }   // digit y of the column c
+
+    __device__ static uint32_t piece_off(uint32_t v) { return ((v >> 6) & 3u) * 32u + (v >> 8) * 16u; }
+
+    // DMA of slot (section Y, group g) of the tile at b0: wave w fills 1 KiB blocks
+    // [2w, 2w+2) of every real node region.  Returns the instructions issued.
+    template <int Y>
+    __device__ static void dma(const BsArgs &a, uint32_t slot_lds, int wave, int lane, uint32_t b0, int g) {
+        const uint32_t sc = uint32_t(a.sc);
+        uint32_t vl = v6::inv_d(uint32_t(lane));
+        asm volatile("" : "+v"(vl));
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            if constexpr (node < KD) {
+#pragma unroll
+                for (int i = 0; i < DMA_PER_NODE; i++) {
+                    const uint32_t blk = uint32_t(wave * DMA_PER_NODE + i);
+                    const uint32_t v = vl ^ v6::inv_d((blk << 6) ^ v6::hbank(x));
+                    uint32_t pos = b0 + piece_off(v);
+                    if (pos + 16u > sc) pos = sc - 16u;  // ragged: patched after landing
+                    const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
+                    dma16(slot_lds + uint32_t(x * NODE_BYTES) + blk * 1024u, a.data[node], layer * sc + pos);
+                }
+            }
+        });
+    }
+    template <int Y>
+    __device__ static void patch(const BsArgs &a, uint8_t *slot, int wave, int lane, uint32_t b0, int g) {
+        const uint32_t sc = uint32_t(a.sc);
+        const uint32_t vl = v6::inv_d(uint32_t(lane));
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            if constexpr (node < KD) {
+#pragma unroll
+                for (int i = 0; i < DMA_PER_NODE; i++) {
+                    const uint32_t blk = uint32_t(wave * DMA_PER_NODE + i);
+                    const uint32_t v = vl ^ v6::inv_d((blk << 6) ^ v6::hbank(x));
+                    const uint32_t pos = b0 + piece_off(v);
+                    if (pos < sc && pos + 16u > sc) {  // 8 valid bytes (sc is a multiple of 8)
+                        const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
+                        const uint2 gv = *reinterpret_cast<const uint2 *>(a.data[node] + layer * sc + pos);
+                        *reinterpret_cast<uint4 *>(slot + x * NODE_BYTES + blk * 1024 + lane * 16) =
+                            make_uint4(gv.x, gv.y, 0u, 0u);
+                    }
+                }
+            }
+        });
+    }
+    __device__ static void dma_any(int y, const BsArgs &a, uint32_t slot_lds, int wave, int lane, uint32_t b0, int g) {
+        if (y == 0) dma<0>(a, slot_lds, wave, lane, b0, g);
+        else if (y == 1) dma<1>(a, slot_lds, wave, lane, b0, g);
+        else dma<2>(a, slot_lds, wave, lane, b0, g);
+    }
+    __device__ static void patch_any(int y, const BsArgs &a, uint8_t *slot, int wave, int lane, uint32_t b0, int g) {
+        if (y == 0) patch<0>(a, slot, wave, lane, b0, g);
+        else if (y == 1) patch<1>(a, slot, wave, lane, b0, g);
+        else patch<2>(a, slot, wave, lane, b0, g);
+    }
+
+    __device__ static void read32(const uint8_t *p0, const uint8_t *p1, uint32_t (&d)[8]) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(p0), v1 = *reinterpret_cast<const uint4 *>(p1);
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+
+    template <int BO>
+    static constexpr uint64_t pft_mask() {
+        return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
+    }
+
+    // One step: section Y of the lane's layer z = 4c + g from the slot -> acc.
+    template <int Y>
+    __device__ static void section(const uint8_t *slot, int c, int part, uint32_t (&acc)[Q * 8]) {
+        constexpr int sh = dshift(Y);
+        constexpr uint32_t FD = v6::fwd_c(1u << 8);
+        const int cy = (c >> sh) & 3;
+        const bool creal = (Y * Q + cy) < KD;
+        const uint32_t fown = v6::fwd_d(uint32_t(c) | uint32_t(part << 6));
+        const uint32_t fcl = v6::fwd_d(uint32_t(c & ~(3 << sh)) | uint32_t(part << 6)) ^ v6::hbank_d(uint32_t(cy));
+        const uint8_t *cbase = slot + cy * NODE_BYTES;
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t o[8], cv[8];
+            if constexpr (Y * Q + x < KD) {
+                const uint32_t po = fown ^ v6::hbank(x);
+                read32(slot + x * NODE_BYTES + 16u * po, slot + x * NODE_BYTES + 16u * (po ^ FD), o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) o[w] = 0;
+            }
+            const uint32_t pc = fcl ^ v6::fwd_c(uint32_t(x) << sh);
+            if (creal) {
+                read32(cbase + 16u * pc, cbase + 16u * (pc ^ FD), cv);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) cv[w] = 0;
+            }
+            const uint32_t keep = (creal && x != cy) ? 0xffffffffu : 0u;
+            const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+            uint32_t u[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+            transpose8(u);
+            sfor<Q>([&](auto pc_) BS_INL {
+                constexpr int p = decltype(pc_)::value;
+                sfor<8>([&](auto bc) BS_INL {
+                    constexpr int bo = decltype(bc)::value;
+                    constexpr uint64_t mk = plane_mask(S::RS.g[p][Y * Q + x], bo, 0);
+                    acc[p * 8 + bo] = xor_sel<mk, (Y > 0 || x > 0)>(acc[p * 8 + bo], u);
+                });
+            });
+        });
+    }
+
+    // Parity output C (8 planes) -> bytes -> HBM at parity node x, layer z.
+    template <int X>
+    __device__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, uint32_t pos, bool ragged, int nv) {
+        transpose8(cv);
+        uint8_t *p = a.par[X] + z * uint32_t(a.sc) + pos;
+        if (!ragged) {
+            st16(p, cv[0], cv[1], cv[2], cv[3]);
+            st16(p + 16, cv[4], cv[5], cv[6], cv[7]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(cv[2 * i], cv[2 * i + 1]);
+        }
+    }
+    // PFT pair: C = det^-1 (u + gamma * ustar)
+    __device__ static void pft(const uint32_t *u, const uint32_t *us, uint32_t (&cv)[8]) {
+        uint32_t in[16];
+#pragma unroll
+        for (int w = 0; w < 8; w++) { in[w] = u[w]; in[8 + w] = us[w]; }
+        sfor<8>([&](auto bc) BS_INL {
+            cv[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
+        });
+    }
+
+    struct Hold {  // U[p][z(h)] for later PFT pairs: h01 = U[1][z0], ...
+        uint32_t h01[8], h02[8], h03[8], h12[8], h13[8], h23[8];
+    };
+
+    // Group g finished: red vertex C[g][z_g] = U, and the PFT pairs with groups h < g.
+    template <int G>
+    __device__ static void end_group(const BsArgs &a, const uint32_t (&acc)[Q * 8], Hold &H, int c, uint32_t pos,
+                                     bool ragged, int nv) {
+        const uint32_t zg = uint32_t(c * 4 + G);
+        uint32_t cv[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) cv[w] = acc[G * 8 + w];
+        put<G>(a, cv, zg, pos, ragged, nv);
+        auto pair = [&](const uint32_t *uh_at_g, const uint32_t *ug_at_h, auto hc) BS_INL {
+            constexpr int h = decltype(hc)::value;
+            const uint32_t zh = uint32_t(c * 4 + h);
+            uint32_t c1[8], c2[8];
+            pft(uh_at_g, ug_at_h, c1);  // C[h][z_g]
+            put<h>(a, c1, zg, pos, ragged, nv);
+            pft(ug_at_h, uh_at_g, c2);  // C[g][z_h]
+            put<G>(a, c2, zh, pos, ragged, nv);
+        };
+        if constexpr (G == 0) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) { H.h01[w] = acc[8 + w]; H.h02[w] = acc[16 + w]; H.h03[w] = acc[24 + w]; }
+        } else if constexpr (G == 1) {
+            pair(acc + 0, H.h01, std::integral_constant<int, 0>{});
+#pragma unroll
+            for (int w = 0; w < 8; w++) { H.h12[w] = acc[16 + w]; H.h13[w] = acc[24 + w]; }
+        } else if constexpr (G == 2) {
+            pair(acc + 0, H.h02, std::integral_constant<int, 0>{});
+            pair(acc + 8, H.h12, std::integral_constant<int, 1>{});
+#pragma unroll
+            for (int w = 0; w < 8; w++) H.h23[w] = acc[24 + w];
+        } else {
+            pair(acc + 0, H.h03, std::integral_constant<int, 0>{});
+            pair(acc + 8, H.h13, std::integral_constant<int, 1>{});
+            pair(acc + 16, H.h23, std::integral_constant<int, 2>{});
+        }
+    }
+};
+
+template <int KD, int M>
+__global__ __launch_bounds__((Bs6Kernel<KD, M>::BLOCK)) void k_bs6_encode(BsArgs a) {
+    using Kn = Bs6Kernel<KD, M>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c = int(threadIdx.x) >> 2, part = int(threadIdx.x) & 3;
+    const uint32_t lds0 = lds_addr_of(smem);
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    // tiles of this workgroup: xcd * tpx + slot + k * nslots
+    int ntile = 0;
+    for (uint32_t tix = slot; tix < a.tiles_per_xcd && xcd * a.tiles_per_xcd + tix < a.ntiles; tix += a.nslots) ntile++;
+    if (ntile == 0) return;
+    const int nsteps = ntile * Kn::STEPS;
+    auto tile_b0 = [&](int k) { return (xcd * a.tiles_per_xcd + slot + uint32_t(k) * a.nslots) * uint32_t(Kn::W); };
+    // counted waits: T = VMEM instructions issued so far by this wave; mk[j] = T right
+    // after the DMA of slot (s + j) was issued (j = 0 .. AHEAD-1)
+    int Tn = 0, mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
+    static_assert(Kn::AHEAD == 4, "mark shift register has 4 entries");
+    auto issue = [&](int s) {
+        if (s < nsteps) {
+            const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
+            Kn::dma_any(y, a, lds0 + uint32_t((s % Kn::RING) * Kn::SLOT), wave, lane, tile_b0(k), g);
+            Tn += Kn::ndma(y);
+        }
+        mk0 = mk1; mk1 = mk2; mk2 = mk3; mk3 = Tn;
+    };
+    for (int s = 0; s < Kn::AHEAD; s++) issue(s);
+    uint32_t acc[Kn::Q * 8];
+    typename Kn::Hold H;
+    const uint32_t sc = uint32_t(a.sc);
+    for (int s = 0; s < nsteps; s++) {
+        const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
+        const uint32_t b0 = tile_b0(k);
+        const bool ragged = uint64_t(b0) + Kn::W > a.sc;
+        uint8_t *slotp = smem + (s % Kn::RING) * Kn::SLOT;
+        if (ragged) {  // plain (uncounted) stores may be in flight: wait for everything
+            wait_vm_n<0>();
+            Kn::patch_any(y, a, slotp, wave, lane, b0, g);
+        } else {
+            wait_vm_rt(Tn - mk0);
+        }
+        lds_barrier();
+        issue(s + Kn::AHEAD);  // refills the slot every wave finished reading last step
+        if (y == 0) Kn::template section<0>(slotp, c, part, acc);
+        else if (y == 1) Kn::template section<1>(slotp, c, part, acc);
+        else Kn::template section<2>(slotp, c, part, acc);
+        if (y == 2) {
+            const uint32_t pos = b0 + uint32_t(32 * part);
+            const int nv = pos >= sc ? 0 : ((sc - pos) / 8 > 4 ? 4 : int((sc - pos) / 8));
+            if (g == 0) Kn::template end_group<0>(a, acc, H, c, pos, ragged, nv);
+            else if (g == 1) Kn::template end_group<1>(a, acc, H, c, pos, ragged, nv);
+            else if (g == 2) Kn::template end_group<2>(a, acc, H, c, pos, ragged, nv);
+            else Kn::template end_group<3>(a, acc, H, c, pos, ragged, nv);
+            Tn += Kn::stores(g);
+        }
+    }
+    wait_vm0();
+}
+
+}  // namespace bs
+}  // namespace clay

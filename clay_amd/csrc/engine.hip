@@ -28,6 +28,7 @@
 #include "code.hpp"
 #include "gf256.hpp"
 #include "bitslice.hpp"
+#include "bitslice6.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -611,6 +612,90 @@ static Error launch_bs4(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
 }
 
 template <int KD, int M>
+static Error launch_bs5(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
+                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::Bs5Kernel<KD, M>;
+    using S = typename Kn::S;
+    const clay_code_t &c = cs.code;
+    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
+    // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 64
+    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 64) return Error{};
+    for (int p = 0; p < M; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    static bool attr[64] = {};
+    int dev = 0;
+    CLAY_HIP(hipGetDevice(&dev));
+    if (!attr[dev]) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs5_encode<KD, M>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
+        attr[dev] = true;
+    }
+    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::BsArgs a{};
+        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
+        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
+        a.sc = sc;
+        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
+        a.tiles_per_xcd = (a.ntiles + 7) / 8;
+        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
+        a.nslots = std::min(max_slots, a.tiles_per_xcd);
+        bs::k_bs5_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        CLAY_HIP(hipGetLastError());
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "bitsliced5-k%dm%d-w%d", KD, M, Kn::W);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
+template <int KD, int M>
+static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
+                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::Bs6Kernel<KD, M>;
+    using S = typename Kn::S;
+    const clay_code_t &c = cs.code;
+    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
+    // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 64
+    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 16) return Error{};
+    for (int p = 0; p < M; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    static bool attr[64] = {};
+    int dev = 0;
+    CLAY_HIP(hipGetDevice(&dev));
+    if (!attr[dev]) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
+        attr[dev] = true;
+    }
+    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::BsArgs a{};
+        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
+        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
+        a.sc = sc;
+        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
+        a.tiles_per_xcd = (a.ntiles + 7) / 8;
+        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
+        a.nslots = std::min(max_slots, a.tiles_per_xcd);
+        bs::k_bs6_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        CLAY_HIP(hipGetLastError());
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "bitsliced6-k%dm%d-w%d", KD, M, Kn::W);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
+template <int KD, int M>
 static Error launch_bs3(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
                         size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
     using Kn = bs::Bs3Kernel<KD, M>;
@@ -668,6 +753,14 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     CLAY_HIP(hipGetDeviceProperties(&prop, dev));
     Error e;
     const int key = int(c.k * 100 + c.m);
+    if (g_encode_mode == 8) {  // v6 (128-byte tiles, column-per-lane, 5-slot ring)
+        if (key == 1004) e = launch_bs6<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+        if (e || *done || g_encode_mode == 8) return e;
+    }
+    if (g_encode_mode == 7) {  // v5 (register accumulators, node-slot ring)
+        if (key == 1004) e = launch_bs5<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+        if (e || *done || g_encode_mode == 7) return e;
+    }
     if (g_encode_mode == 6 || (g_encode_mode == 0 && g_bs_pg == 0)) {  // v4 (16-byte LDS-DMA, conflict-free stage / accumulator)
         if (key == 1004) e = launch_bs4<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
         if (e || *done || g_encode_mode == 6) return e;

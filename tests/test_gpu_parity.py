@@ -88,9 +88,11 @@ def test_bitsliced23_encode_matches_oracle(oracle_mod, cfg, scale, variant):
     assert np.array_equal(got, ref), (cfg, scale)
 
 
+@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6"])
 @pytest.mark.parametrize("sc", [64, 72, 104, 128, 1064, 6440, 64 * 300 + 40, 64 * 2000 + 8])
-def test_bitsliced4_encode_matches_oracle(oracle_mod, sc):
-    """v4 (16-byte LDS-DMA, swizzled stage / accumulator), (10,4,13) only.  sc % 16 == 8
+def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
+    """v4 (16-byte LDS-DMA, swizzled stage / accumulator) and v5 (register
+    accumulators, node-slot ring), (10,4,13) only.  sc % 16 == 8
     sizes put an 8-valid-byte piece in the last tile (DMA'd clamped, patched in LDS);
     64 * 2000 + 8 has more tiles than workgroups (cross-tile prefetch)."""
     k, m, d = 10, 4, 13
@@ -99,9 +101,9 @@ def test_bitsliced4_encode_matches_oracle(oracle_mod, sc):
     data = rand_bytes(sc, n)
     ref = o.encode_array(data)
     assert ref.shape[1] == c.sub_chunk_no * sc
-    set_encode_path("bitsliced4")
+    set_encode_path(variant)
     got = c.encode_array(data)
-    assert last_encode_path().startswith("bitsliced4"), last_encode_path()
+    assert last_encode_path().startswith(variant), last_encode_path()
     assert np.array_equal(got, ref), sc
 
 
