@@ -97,53 +97,72 @@ constexpr GfLin<NB> make_gflin(const uint32_t (&bm)[4]) {
 }
 
 namespace v6 {
-constexpr uint32_t BM[4] = {0xf3, 0x85, 0x17a, 0x1e5};  // over v = c | part << 6 | d << 8
-constexpr uint32_t HM[4] = {0, 0, 3, 2};                // over the slot-local node x
-constexpr GfLin<9> LIN = make_gflin<9>(BM);
 constexpr int par32(uint32_t v) {
     int p = 0;
     for (; v; v &= v - 1) p ^= 1;
     return p;
 }
-constexpr uint32_t fwd_c(uint32_t v) {
-    uint32_t p = 0;
-    for (int i = 0; i < 9; i++)
-        if ((v >> i) & 1) p ^= LIN.fwd[i];
-    return p;
-}
-constexpr uint32_t inv_c(uint32_t p) {
-    uint32_t v = 0;
-    for (int i = 0; i < 9; i++)
-        if ((p >> i) & 1) v ^= LIN.inv[i];
-    return v;
-}
-constexpr uint32_t hbank(int x) {
-    uint32_t b = 0;
-    for (int o = 0; o < 4; o++) b |= uint32_t(par32(uint32_t(x) & HM[o])) << o;
-    return b;
-}
-static_assert(inv_c(fwd_c(0x1A5)) == 0x1A5 && inv_c(fwd_c(0x0FF)) == 0x0FF, "v6 layout bijection");
-static_assert((fwd_c(0x1FF) & 15) == ((par32(0x1FF & BM[0])) | (par32(0x1FF & BM[1]) << 1) |
-                                      (par32(0x1FF & BM[2]) << 2) | (par32(0x1FF & BM[3]) << 3)),
-              "bank bits of the piece index");
-__device__ __forceinline__ uint32_t fwd_d(uint32_t v) {
-    uint32_t p = 0;
+// Slot image per tile width: piece v = c | part << 6 | d << (6 + log2 PARTS);
+// BM over v, HM over the slot-local node x (tools/v6_layout_search.py, v7_layout_search.py)
+template <int PARTS>
+struct Layout;
+template <>
+struct Layout<4> {
+    static constexpr int PB = 2, NB = 9;
+    static constexpr uint32_t BM[4] = {0xf3, 0x85, 0x17a, 0x1e5};
+    static constexpr uint32_t HM[4] = {0, 0, 3, 2};
+};
+template <>
+struct Layout<8> {
+    static constexpr int PB = 3, NB = 10;
+    static constexpr uint32_t BM[4] = {0x269, 0x6, 0x2b4, 0x87};
+    static constexpr uint32_t HM[4] = {2, 2, 2, 3};
+};
+template <int PARTS>
+struct Map {
+    using L = Layout<PARTS>;
+    static constexpr int NB = L::NB;
+    static constexpr GfLin<NB> LIN = make_gflin<NB>(L::BM);
+    static constexpr uint32_t fwd_c(uint32_t v) {
+        uint32_t p = 0;
+        for (int i = 0; i < NB; i++)
+            if ((v >> i) & 1) p ^= LIN.fwd[i];
+        return p;
+    }
+    static constexpr uint32_t inv_c(uint32_t p) {
+        uint32_t v = 0;
+        for (int i = 0; i < NB; i++)
+            if ((p >> i) & 1) v ^= LIN.inv[i];
+        return v;
+    }
+    static constexpr uint32_t hbank(int x) {
+        uint32_t b = 0;
+        for (int o = 0; o < 4; o++) b |= uint32_t(par32(uint32_t(x) & L::HM[o])) << o;
+        return b;
+    }
+    static_assert(inv_c(fwd_c(0x1A5)) == 0x1A5 && inv_c(fwd_c(0x0FF)) == 0x0FF, "v6 layout bijection");
+    static_assert((fwd_c(0x1FF) & 15) == uint32_t(par32(0x1FF & L::BM[0]) | (par32(0x1FF & L::BM[1]) << 1) |
+                                                  (par32(0x1FF & L::BM[2]) << 2) | (par32(0x1FF & L::BM[3]) << 3)),
+                  "bank bits of the piece index");
+    __device__ static __forceinline__ uint32_t fwd_d(uint32_t v) {
+        uint32_t p = 0;
 #pragma unroll
-    for (int i = 0; i < 9; i++) p ^= ((v >> i) & 1) ? uint32_t(LIN.fwd[i]) : 0u;
-    return p;
-}
-__device__ __forceinline__ uint32_t inv_d(uint32_t p) {
-    uint32_t v = 0;
+        for (int i = 0; i < NB; i++) p ^= ((v >> i) & 1) ? uint32_t(LIN.fwd[i]) : 0u;
+        return p;
+    }
+    __device__ static __forceinline__ uint32_t inv_d(uint32_t p) {
+        uint32_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 9; i++) v ^= ((p >> i) & 1) ? uint32_t(LIN.inv[i]) : 0u;
-    return v;
-}
-__device__ __forceinline__ uint32_t hbank_d(uint32_t x) {
-    uint32_t b = 0;
+        for (int i = 0; i < NB; i++) v ^= ((p >> i) & 1) ? uint32_t(LIN.inv[i]) : 0u;
+        return v;
+    }
+    __device__ static __forceinline__ uint32_t hbank_d(uint32_t x) {
+        uint32_t b = 0;
 #pragma unroll
-    for (int o = 0; o < 4; o++) b |= uint32_t(__builtin_popcount(x & HM[o]) & 1) << o;
-    return b;
-}
+        for (int o = 0; o < 4; o++) b |= uint32_t(__builtin_popcount(x & L::HM[o]) & 1) << o;
+        return b;
+    }
+};
 }  // namespace v6
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field)
@@ -158,17 +177,19 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     }
 }
 
-template <int KD, int M>
+template <int KD, int M, int PARTS>
 struct Bs6Kernel {
     using S = Shape<KD, M>;
+    using MP = v6::Map<PARTS>;
+    static constexpr int PB = v6::Layout<PARTS>::PB;
     static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
     static_assert(KD == 10 && M == 4 && Q == 4 && T == 4 && ALPHA == 256,
                   "v6 slot layout is derived for (10,4,13)");
-    static constexpr int W = 128, PARTS = 4, COLS = ALPHA / Q, BLOCK = COLS * PARTS, WAVES = BLOCK / 64;
-    static constexpr int NODE_BYTES = COLS * W;            // 8 KiB: one node of one (Y, g) slot
-    static constexpr int SLOT = Q * NODE_BYTES;            // 32 KiB
-    static constexpr int RING = 5;
-    static constexpr int LDS_BYTES = RING * SLOT;          // 160 KiB
+    static constexpr int W = 32 * PARTS, COLS = ALPHA / Q, BLOCK = COLS * PARTS, WAVES = BLOCK / 64;
+    static constexpr int NODE_BYTES = COLS * W;            // one node of one (Y, g) slot
+    static constexpr int SLOT = Q * NODE_BYTES;            // 32 KiB (W 128) / 64 KiB (W 256)
+    static constexpr int RING = (160 * 1024) / SLOT;       // 5 / 2
+    static constexpr int LDS_BYTES = RING * SLOT;
     static constexpr int AHEAD = RING - 1;                 // slots in flight ahead of the read
     static constexpr int STEPS = (T - 1) * Q;              // (section, group) steps per tile
     static constexpr int DMA_PER_NODE = NODE_BYTES / 1024 / WAVES;  // per wave: 2
@@ -178,14 +199,16 @@ struct Bs6Kernel {
     static constexpr int stores(int g) { return (1 + 2 * g) * 2; }  // dwordx4 per lane at group end
     static constexpr int dshift(int y) { return 2 * (T - 2 - y); }   // digit y of the column c
 
-    __device__ static uint32_t piece_off(uint32_t v) { return ((v >> 6) & 3u) * 32u + (v >> 8) * 16u; }
+    __device__ static uint32_t piece_off(uint32_t v) {
+        return ((v >> 6) & uint32_t(PARTS - 1)) * 32u + (v >> (6 + PB)) * 16u;
+    }
 
     // DMA of slot (section Y, group g) of the tile at b0: wave w fills 1 KiB blocks
     // [2w, 2w+2) of every real node region.  Returns the instructions issued.
     template <int Y>
     __device__ static void dma(const BsArgs &a, uint32_t slot_lds, int wave, int lane, uint32_t b0, int g) {
         const uint32_t sc = uint32_t(a.sc);
-        uint32_t vl = v6::inv_d(uint32_t(lane));
+        uint32_t vl = MP::inv_d(uint32_t(lane));
         asm volatile("" : "+v"(vl));
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
@@ -194,7 +217,7 @@ struct Bs6Kernel {
 #pragma unroll
                 for (int i = 0; i < DMA_PER_NODE; i++) {
                     const uint32_t blk = uint32_t(wave * DMA_PER_NODE + i);
-                    const uint32_t v = vl ^ v6::inv_d((blk << 6) ^ v6::hbank(x));
+                    const uint32_t v = vl ^ MP::inv_d((blk << 6) ^ MP::hbank(x));
                     uint32_t pos = b0 + piece_off(v);
                     if (pos + 16u > sc) pos = sc - 16u;  // ragged: patched after landing
                     const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
@@ -206,7 +229,7 @@ struct Bs6Kernel {
     template <int Y>
     __device__ static void patch(const BsArgs &a, uint8_t *slot, int wave, int lane, uint32_t b0, int g) {
         const uint32_t sc = uint32_t(a.sc);
-        const uint32_t vl = v6::inv_d(uint32_t(lane));
+        const uint32_t vl = MP::inv_d(uint32_t(lane));
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
             constexpr int node = Y * Q + x;
@@ -214,7 +237,7 @@ struct Bs6Kernel {
 #pragma unroll
                 for (int i = 0; i < DMA_PER_NODE; i++) {
                     const uint32_t blk = uint32_t(wave * DMA_PER_NODE + i);
-                    const uint32_t v = vl ^ v6::inv_d((blk << 6) ^ v6::hbank(x));
+                    const uint32_t v = vl ^ MP::inv_d((blk << 6) ^ MP::hbank(x));
                     const uint32_t pos = b0 + piece_off(v);
                     if (pos < sc && pos + 16u > sc) {  // 8 valid bytes (sc is a multiple of 8)
                         const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
@@ -252,23 +275,23 @@ struct Bs6Kernel {
     template <int Y>
     __device__ static void section(const uint8_t *slot, int c, int part, uint32_t (&acc)[Q * 8]) {
         constexpr int sh = dshift(Y);
-        constexpr uint32_t FD = v6::fwd_c(1u << 8);
+        constexpr uint32_t FD = MP::fwd_c(1u << (6 + PB));
         const int cy = (c >> sh) & 3;
         const bool creal = (Y * Q + cy) < KD;
-        const uint32_t fown = v6::fwd_d(uint32_t(c) | uint32_t(part << 6));
-        const uint32_t fcl = v6::fwd_d(uint32_t(c & ~(3 << sh)) | uint32_t(part << 6)) ^ v6::hbank_d(uint32_t(cy));
+        const uint32_t fown = MP::fwd_d(uint32_t(c) | uint32_t(part << 6));
+        const uint32_t fcl = MP::fwd_d(uint32_t(c & ~(3 << sh)) | uint32_t(part << 6)) ^ MP::hbank_d(uint32_t(cy));
         const uint8_t *cbase = slot + cy * NODE_BYTES;
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
             uint32_t o[8], cv[8];
             if constexpr (Y * Q + x < KD) {
-                const uint32_t po = fown ^ v6::hbank(x);
+                const uint32_t po = fown ^ MP::hbank(x);
                 read32(slot + x * NODE_BYTES + 16u * po, slot + x * NODE_BYTES + 16u * (po ^ FD), o);
             } else {
 #pragma unroll
                 for (int w = 0; w < 8; w++) o[w] = 0;
             }
-            const uint32_t pc = fcl ^ v6::fwd_c(uint32_t(x) << sh);
+            const uint32_t pc = fcl ^ MP::fwd_c(uint32_t(x) << sh);
             if (creal) {
                 read32(cbase + 16u * pc, cbase + 16u * (pc ^ FD), cv);
             } else {
@@ -358,12 +381,12 @@ struct Bs6Kernel {
     }
 };
 
-template <int KD, int M>
-__global__ __launch_bounds__((Bs6Kernel<KD, M>::BLOCK)) void k_bs6_encode(BsArgs a) {
-    using Kn = Bs6Kernel<KD, M>;
+template <int KD, int M, int PARTS>
+__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode(BsArgs a) {
+    using Kn = Bs6Kernel<KD, M, PARTS>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int c = int(threadIdx.x) >> 2, part = int(threadIdx.x) & 3;
+    const int c = int(threadIdx.x) >> Kn::PB, part = int(threadIdx.x) & (PARTS - 1);
     const uint32_t lds0 = lds_addr_of(smem);
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
     // tiles of this workgroup: xcd * tpx + slot + k * nslots
@@ -374,15 +397,17 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M>::BLOCK)) void k_bs6_encode(BsArgs
     auto tile_b0 = [&](int k) { return (xcd * a.tiles_per_xcd + slot + uint32_t(k) * a.nslots) * uint32_t(Kn::W); };
     // counted waits: T = VMEM instructions issued so far by this wave; mk[j] = T right
     // after the DMA of slot (s + j) was issued (j = 0 .. AHEAD-1)
-    int Tn = 0, mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
-    static_assert(Kn::AHEAD == 4, "mark shift register has 4 entries");
+    int Tn = 0, mk[4] = {0, 0, 0, 0};
+    static_assert(Kn::AHEAD >= 1 && Kn::AHEAD <= 4, "mark shift register has 4 entries");
     auto issue = [&](int s) {
         if (s < nsteps) {
             const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
             Kn::dma_any(y, a, lds0 + uint32_t((s % Kn::RING) * Kn::SLOT), wave, lane, tile_b0(k), g);
             Tn += Kn::ndma(y);
         }
-        mk0 = mk1; mk1 = mk2; mk2 = mk3; mk3 = Tn;
+#pragma unroll
+        for (int j = 0; j + 1 < Kn::AHEAD; j++) mk[j] = mk[j + 1];
+        mk[Kn::AHEAD - 1] = Tn;
     };
     for (int s = 0; s < Kn::AHEAD; s++) issue(s);
     uint32_t acc[Kn::Q * 8];
@@ -397,7 +422,7 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M>::BLOCK)) void k_bs6_encode(BsArgs
             wait_vm_n<0>();
             Kn::patch_any(y, a, slotp, wave, lane, b0, g);
         } else {
-            wait_vm_rt(Tn - mk0);
+            wait_vm_rt(Tn - mk[0]);
         }
         lds_barrier();
         issue(s + Kn::AHEAD);  // refills the slot every wave finished reading last step

@@ -653,10 +653,10 @@ static Error launch_bs5(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     return Error{};
 }
 
-template <int KD, int M>
+template <int KD, int M, int PARTS>
 static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
                         size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs6Kernel<KD, M>;
+    using Kn = bs::Bs6Kernel<KD, M, PARTS>;
     using S = typename Kn::S;
     const clay_code_t &c = cs.code;
     if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
@@ -670,7 +670,7 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     int dev = 0;
     CLAY_HIP(hipGetDevice(&dev));
     if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M>),
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
         attr[dev] = true;
     }
@@ -684,7 +684,7 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
         a.tiles_per_xcd = (a.ntiles + 7) / 8;
         const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
         a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs6_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        bs::k_bs6_encode<KD, M, PARTS><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
         CLAY_HIP(hipGetLastError());
         t_last_launches++;
     }
@@ -753,8 +753,13 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     CLAY_HIP(hipGetDeviceProperties(&prop, dev));
     Error e;
     const int key = int(c.k * 100 + c.m);
-    if (g_encode_mode == 8) {  // v6 (128-byte tiles, column-per-lane, 5-slot ring)
-        if (key == 1004) e = launch_bs6<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+    // v6 (column-per-lane, PFT without exchange): 256-byte tiles / 2-slot ring by default
+    // (auto's first choice for (10,4,13)); tile override 4 = 128-byte tiles / 5-slot ring
+    if (g_encode_mode == 8 || (g_encode_mode == 0 && g_bs_pg == 0)) {
+        if (key == 1004) {
+            if (g_bs_pg == 4) e = launch_bs6<10, 4, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
+            else e = launch_bs6<10, 4, 8>(cs, prop, data, par, n_stripes, sc, stream, done);
+        }
         if (e || *done || g_encode_mode == 8) return e;
     }
     if (g_encode_mode == 7) {  // v5 (register accumulators, node-slot ring)

@@ -166,9 +166,11 @@ int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int devic
  * 8-byte aligned, else the byte-sliced fused kernel when parity is one y-section,
  * else the staged engine), 1 = force staged, 2 = require byte-sliced fused,
  * 3 = require bit-sliced v1 (register loads), 4 = v2 (4-byte LDS-DMA staging),
- * 5 = v3 (register accumulators), 6 = v4 (16-byte LDS-DMA, conflict-free LDS;
- * auto's first choice for (10,4,13)).  Bits 8..15: v1 tile override (0 = default;
- * a non-zero override also keeps auto on v1).  Returns the previous low-byte mode. */
+ * 5 = v3 (register accumulators), 6 = v4 (16-byte LDS-DMA, conflict-free LDS),
+ * 7 = v5 (node-slot ring), 8 = v6 (column-per-lane, 256-byte tiles; auto's first
+ * choice for (10,4,13), then v4).  Bits 8..15: tile override (v1: lanes per value;
+ * v6: 4 = 128-byte tiles; a non-zero override keeps auto off v4/v6).  Returns the
+ * previous low-byte mode. */
 int clay_set_encode_path(int mode);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */

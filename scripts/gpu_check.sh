@@ -8,6 +8,11 @@ TAG=${1:-run}
 echo "[$(date +%T)] pytest -m gpu (not slow)"
 timeout -k 10 600 python -m pytest tests -m "gpu and not slow" -x -q > gpurun_out/${TAG}_pytest_fast.log 2>&1 || { echo "pytest fast failed rc=$?"; tail -40 gpurun_out/${TAG}_pytest_fast.log; exit 1; }
 tail -3 gpurun_out/${TAG}_pytest_fast.log
+if [ -z "$SKIP_SLOW" ]; then
+echo "[$(date +%T)] pytest -m 'gpu and slow' (BASELINE sizes)"
+timeout -k 10 900 python -m pytest tests -m "gpu and slow" -x -q > gpurun_out/${TAG}_pytest_slow.log 2>&1 || { echo "pytest slow failed rc=$?"; tail -40 gpurun_out/${TAG}_pytest_slow.log; exit 1; }
+tail -3 gpurun_out/${TAG}_pytest_slow.log
+fi
 echo "[$(date +%T)] smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -2 gpurun_out/${TAG}_smoke.log
@@ -18,4 +23,8 @@ echo "[$(date +%T)] rocprofv3 kernel trace"
 export TMPDIR=/tmp
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o enc --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-verify --no-host-path --cpu-seconds 0 ) > gpurun_out/${TAG}_rocprof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/${TAG}_rocprof.log; exit 1; }
 find gpurun_out/${TAG}_prof -name "*stats*" | head
+if [ -n "$PMC" ]; then
+echo "[$(date +%T)] PMC passes"
+bash scripts/prof_pmc.sh ${TAG}_pmc auto 0 || { echo "pmc failed"; exit 1; }
+fi
 echo "[$(date +%T)] done"

@@ -88,7 +88,7 @@ def test_bitsliced23_encode_matches_oracle(oracle_mod, cfg, scale, variant):
     assert np.array_equal(got, ref), (cfg, scale)
 
 
-@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6"])
+@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6", "bitsliced6:4"])
 @pytest.mark.parametrize("sc", [64, 72, 104, 128, 1064, 6440, 64 * 300 + 40, 64 * 2000 + 8])
 def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
     """v4 (16-byte LDS-DMA, swizzled stage / accumulator) and v5 (register
@@ -101,9 +101,10 @@ def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
     data = rand_bytes(sc, n)
     ref = o.encode_array(data)
     assert ref.shape[1] == c.sub_chunk_no * sc
-    set_encode_path(variant)
+    name, _, tile = variant.partition(":")
+    set_encode_path(name, int(tile or 0))
     got = c.encode_array(data)
-    assert last_encode_path().startswith(variant), last_encode_path()
+    assert last_encode_path().startswith(name), last_encode_path()
     assert np.array_equal(got, ref), sc
 
 
@@ -271,11 +272,17 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
     assert chunk == 107_374_592
     ref = o.encode_array(data)
     dev = torch.from_numpy(ref[:10].copy()).cuda()
-    par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
-    c.encode_device([dev[i] for i in range(10)], [par[i] for i in range(4)], chunk)
-    torch.cuda.synchronize()
-    assert clay_amd.last_encode_path().startswith("fused")
-    assert np.array_equal(par.cpu().numpy(), ref[10:])
+    # every encode kernel at the BASELINE size (sc = 419,432: ragged last tile, 8-byte
+    # aligned sub-chunks), auto first
+    for path, tile, prefix in [("auto", 0, "bitsliced6-k10m4-w256"), ("bitsliced6", 4, "bitsliced6-k10m4-w128"),
+                               ("bitsliced4", 0, "bitsliced4"), ("bitsliced2", 0, "bitsliced2"),
+                               ("fused", 0, "fused")]:
+        par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
+        set_encode_path(path, tile)
+        c.encode_device([dev[i] for i in range(10)], [par[i] for i in range(4)], chunk)
+        torch.cuda.synchronize()
+        assert clay_amd.last_encode_path().startswith(prefix), (path, clay_amd.last_encode_path())
+        assert np.array_equal(par.cpu().numpy(), ref[10:]), path
 
 
 @pytest.mark.slow
