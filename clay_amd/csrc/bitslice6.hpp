@@ -165,6 +165,27 @@ struct Map {
 };
 }  // namespace v6
 
+#ifdef CLAY_STAMPS
+__device__ uint64_t *g_clay_stamps;  // [block][wave][phase] cycle sums (tools/stamp_v6.hip)
+#define CLAY_ST(i)                                              \
+    do {                                                        \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();       \
+        st_acc[i] += t_ - st_prev;                              \
+        st_prev = t_;                                           \
+    } while (0)
+#else
+#define CLAY_ST(i) \
+    do {           \
+    } while (0)
+#endif
+
+// 16-byte store, SGPR base + per-lane 32-bit offset (one VMEM instruction, counted)
+__device__ __forceinline__ void st16s(const uint8_t *sbase, uint32_t voff, uint32_t a, uint32_t b, uint32_t c,
+                                      uint32_t d) {
+    const u32x4 v = {a, b, c, d};
+    asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field)
 __device__ __forceinline__ void wait_vm_rt(int n) {
     switch (n < 63 ? n : 63) {
@@ -177,7 +198,7 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     }
 }
 
-template <int KD, int M, int PARTS>
+template <int KD, int M, int PARTS, bool EARLY>
 struct Bs6Kernel {
     using S = Shape<KD, M>;
     using MP = v6::Map<PARTS>;
@@ -190,7 +211,10 @@ struct Bs6Kernel {
     static constexpr int SLOT = Q * NODE_BYTES;            // 32 KiB (W 128) / 64 KiB (W 256)
     static constexpr int RING = (160 * 1024) / SLOT;       // 5 / 2
     static constexpr int LDS_BYTES = RING * SLOT;
-    static constexpr int AHEAD = RING - 1;                 // slots in flight ahead of the read
+    // slots in flight ahead of the one being read: with EARLY the step pulls its whole slot
+    // into registers and releases it at a second barrier, so the slot just read is refilled
+    // before the compute (RING slots in flight); otherwise it is refilled next step
+    static constexpr int AHEAD = EARLY ? RING : RING - 1;
     static constexpr int STEPS = (T - 1) * Q;              // (section, group) steps per tile
     static constexpr int DMA_PER_NODE = NODE_BYTES / 1024 / WAVES;  // per wave: 2
 
@@ -249,6 +273,30 @@ struct Bs6Kernel {
             }
         });
     }
+    // DMA of node x of slot (section Y, group g) only (DMA_PER_NODE instructions if real)
+    template <int Y, int X>
+    __device__ static void dma_node(const BsArgs &a, uint32_t slot_lds, int wave, uint32_t vl, uint32_t b0, int g) {
+        constexpr int node = Y * Q + X;
+        if constexpr (node < KD) {
+            const uint32_t sc = uint32_t(a.sc);
+#pragma unroll
+            for (int i = 0; i < DMA_PER_NODE; i++) {
+                const uint32_t blk = uint32_t(wave * DMA_PER_NODE + i);
+                const uint32_t v = vl ^ MP::inv_d((blk << 6) ^ MP::hbank(X));
+                uint32_t pos = b0 + piece_off(v);
+                if (pos + 16u > sc) pos = sc - 16u;  // ragged: patched after landing
+                const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
+                dma16(slot_lds + uint32_t(X * NODE_BYTES) + blk * 1024u, a.data[node], layer * sc + pos);
+            }
+        }
+    }
+    template <int X>
+    __device__ static void dma_node_any(int y, const BsArgs &a, uint32_t slot_lds, int wave, uint32_t vl, uint32_t b0,
+                                        int g) {
+        if (y == 0) dma_node<0, X>(a, slot_lds, wave, vl, b0, g);
+        else if (y == 1) dma_node<1, X>(a, slot_lds, wave, vl, b0, g);
+        else dma_node<2, X>(a, slot_lds, wave, vl, b0, g);
+    }
     __device__ static void dma_any(int y, const BsArgs &a, uint32_t slot_lds, int wave, int lane, uint32_t b0, int g) {
         if (y == 0) dma<0>(a, slot_lds, wave, lane, b0, g);
         else if (y == 1) dma<1>(a, slot_lds, wave, lane, b0, g);
@@ -271,59 +319,119 @@ struct Bs6Kernel {
         return plane_mask(S::DINV, BO, 0) | plane_mask(gm(S::DINV, 2), BO, 8);
     }
 
-    // One step: section Y of the lane's layer z = 4c + g from the slot -> acc.
-    template <int Y>
-    __device__ static void section(const uint8_t *slot, int c, int part, uint32_t (&acc)[Q * 8]) {
+    // Per-lane piece indices (loop invariant): own piece, and per data section Y the
+    // companion base (digit Y of c cleared, bank XOR of the companion node folded in).
+    struct LaneC {
+        uint32_t fown;
+        uint32_t fcl[T - 1];
+        int cy[T - 1];
+    };
+    __device__ static LaneC lane_consts(int c, int part) {
+        LaneC L;
+        L.fown = MP::fwd_d(uint32_t(c) | uint32_t(part << 6));
+#pragma unroll
+        for (int y = 0; y < T - 1; y++) {
+            const int sh = dshift(y);
+            L.cy[y] = (c >> sh) & 3;
+            L.fcl[y] = MP::fwd_d(uint32_t(c & ~(3 << sh)) | uint32_t(part << 6)) ^ MP::hbank_d(uint32_t(L.cy[y]));
+        }
+        return L;
+    }
+
+    // Stage reads of section Y for the lane's layer: own value and companion per node x.
+    template <int Y, int X>
+    __device__ static void load_x(const uint8_t *slot, const LaneC &L, uint32_t (&o)[8], uint32_t (&cv)[8]) {
         constexpr int sh = dshift(Y);
         constexpr uint32_t FD = MP::fwd_c(1u << (6 + PB));
-        const int cy = (c >> sh) & 3;
+        const int cy = L.cy[Y];
+        if constexpr (Y * Q + X < KD) {
+            const uint32_t po = L.fown ^ MP::hbank(X);
+            read32(slot + X * NODE_BYTES + 16u * po, slot + X * NODE_BYTES + 16u * (po ^ FD), o);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; w++) o[w] = 0;
+        }
+        const uint32_t pc = L.fcl[Y] ^ MP::fwd_c(uint32_t(X) << sh);
+        if ((Y * Q + cy) < KD) {
+            const uint8_t *cbase = slot + cy * NODE_BYTES;
+            read32(cbase + 16u * pc, cbase + 16u * (pc ^ FD), cv);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; w++) cv[w] = 0;
+        }
+    }
+    // PRT of node x in the byte domain: U = O + gamma * C* (C* masked off for the red
+    // vertex and for shortened companions).
+    template <int Y, int X>
+    __device__ static void prt_x(const uint32_t (&o)[8], const uint32_t (&cv)[8], const LaneC &L, uint32_t (&u)[8]) {
+        const int cy = L.cy[Y];
         const bool creal = (Y * Q + cy) < KD;
-        const uint32_t fown = MP::fwd_d(uint32_t(c) | uint32_t(part << 6));
-        const uint32_t fcl = MP::fwd_d(uint32_t(c & ~(3 << sh)) | uint32_t(part << 6)) ^ MP::hbank_d(uint32_t(cy));
-        const uint8_t *cbase = slot + cy * NODE_BYTES;
-        sfor<Q>([&](auto xc) BS_INL {
-            constexpr int x = decltype(xc)::value;
-            uint32_t o[8], cv[8];
-            if constexpr (Y * Q + x < KD) {
-                const uint32_t po = fown ^ MP::hbank(x);
-                read32(slot + x * NODE_BYTES + 16u * po, slot + x * NODE_BYTES + 16u * (po ^ FD), o);
-            } else {
+        const uint32_t keep = (creal && X != cy) ? 0xffffffffu : 0u;
+        const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
 #pragma unroll
-                for (int w = 0; w < 8; w++) o[w] = 0;
-            }
-            const uint32_t pc = fcl ^ MP::fwd_c(uint32_t(x) << sh);
-            if (creal) {
-                read32(cbase + 16u * pc, cbase + 16u * (pc ^ FD), cv);
-            } else {
-#pragma unroll
-                for (int w = 0; w < 8; w++) cv[w] = 0;
-            }
-            const uint32_t keep = (creal && x != cy) ? 0xffffffffu : 0u;
-            const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
-            uint32_t u[8];
-#pragma unroll
-            for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
-            transpose8(u);
-            sfor<Q>([&](auto pc_) BS_INL {
-                constexpr int p = decltype(pc_)::value;
-                sfor<8>([&](auto bc) BS_INL {
-                    constexpr int bo = decltype(bc)::value;
-                    constexpr uint64_t mk = plane_mask(S::RS.g[p][Y * Q + x], bo, 0);
-                    acc[p * 8 + bo] = xor_sel<mk, (Y > 0 || x > 0)>(acc[p * 8 + bo], u);
-                });
+        for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+    }
+    // bit transpose + RS fold of U[x] into the accumulators.
+    template <int Y, int X>
+    __device__ static void fold_x(uint32_t (&u)[8], uint32_t (&acc)[Q * 8]) {
+        transpose8(u);
+        sfor<Q>([&](auto pc_) BS_INL {
+            constexpr int p = decltype(pc_)::value;
+            sfor<8>([&](auto bc) BS_INL {
+                constexpr int bo = decltype(bc)::value;
+                constexpr uint64_t mk = plane_mask(S::RS.g[p][Y * Q + X], bo, 0);
+                acc[p * 8 + bo] = xor_sel<mk, (Y > 0 || X > 0)>(acc[p * 8 + bo], u);
             });
         });
     }
+    // One step, reads interleaved with compute (the slot stays busy until the next step).
+    // pre(x) runs before node x: the caller issues that node's part of the next slot's
+    // DMA there, so the DMA queue drains while the XOR networks run instead of stalling
+    // every wave in issue right after the barrier.
+    template <int Y, class Pre>
+    __device__ static void section(const uint8_t *slot, const LaneC &L, uint32_t (&acc)[Q * 8], Pre &&pre) {
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            pre(xc);
+            uint32_t o[8], cv[8], u[8];
+            load_x<Y, x>(slot, L, o, cv);
+            prt_x<Y, x>(o, cv, L, u);
+            fold_x<Y, x>(u, acc);
+        });
+    }
+    // EARLY: all of the step's reads + PRT first (U: 32 VGPRs), then the caller
+    // releases the slot and folds.
+    template <int Y>
+    __device__ static void load_prt_all(const uint8_t *slot, const LaneC &L, uint32_t (&u)[Q][8]) {
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            uint32_t o[8], cv[8];
+            load_x<Y, x>(slot, L, o, cv);
+            prt_x<Y, x>(o, cv, L, u[x]);
+        });
+    }
+    template <int Y>
+    __device__ static void fold_all(uint32_t (&u)[Q][8], uint32_t (&acc)[Q * 8]) {
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            fold_x<Y, x>(u[x], acc);
+        });
+    }
 
-    // Parity output C (8 planes) -> bytes -> HBM at parity node x, layer z.
+    // Parity output C (8 planes) -> bytes -> HBM at parity node x, layer z.  Stores use
+    // the SGPR-base + 32-bit offset form; the offset is formed here and kept opaque,
+    // otherwise LICM hoists all 16 (node, layer) 64-bit addresses out of the tile loop.
     template <int X>
     __device__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, uint32_t pos, bool ragged, int nv) {
         transpose8(cv);
-        uint8_t *p = a.par[X] + z * uint32_t(a.sc) + pos;
+        uint32_t off = z * uint32_t(a.sc);
+        asm volatile("" : "+v"(off));
+        off += pos;
         if (!ragged) {
-            st16(p, cv[0], cv[1], cv[2], cv[3]);
-            st16(p + 16, cv[4], cv[5], cv[6], cv[7]);
+            st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
+            st16s(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
         } else {
+            uint8_t *p = a.par[X] + off;
 #pragma unroll
             for (int i = 0; i < 4; i++)
                 if (i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(cv[2 * i], cv[2 * i + 1]);
@@ -339,8 +447,11 @@ struct Bs6Kernel {
         });
     }
 
-    struct Hold {  // U[p][z(h)] for later PFT pairs: h01 = U[1][z0], ...
-        uint32_t h01[8], h02[8], h03[8], h12[8], h13[8], h23[8];
+    // U[p][z(h)] values later PFT pairs need, in four rotating 8-plane registers sets
+    // (never more than four live): after group 0 R0 = U[1][z0], R1 = U[2][z0],
+    // R2 = U[3][z0]; after group 1 R0 = U[2][z1], R3 = U[3][z1]; after group 2 R1 = U[3][z2].
+    struct Hold {
+        uint32_t r[4][8];
     };
 
     // Group g finished: red vertex C[g][z_g] = U, and the PFT pairs with groups h < g.
@@ -361,29 +472,33 @@ struct Bs6Kernel {
             pft(ug_at_h, uh_at_g, c2);  // C[g][z_h]
             put<G>(a, c2, zh, pos, ragged, nv);
         };
+        auto keep = [&](int ri, int p) BS_INL {
+#pragma unroll
+            for (int w = 0; w < 8; w++) H.r[ri][w] = acc[p * 8 + w];
+        };
         if constexpr (G == 0) {
-#pragma unroll
-            for (int w = 0; w < 8; w++) { H.h01[w] = acc[8 + w]; H.h02[w] = acc[16 + w]; H.h03[w] = acc[24 + w]; }
+            keep(0, 1);
+            keep(1, 2);
+            keep(2, 3);
         } else if constexpr (G == 1) {
-            pair(acc + 0, H.h01, std::integral_constant<int, 0>{});
-#pragma unroll
-            for (int w = 0; w < 8; w++) { H.h12[w] = acc[16 + w]; H.h13[w] = acc[24 + w]; }
+            pair(acc + 0, H.r[0], std::integral_constant<int, 0>{});  // U[1][z0]
+            keep(0, 2);
+            keep(3, 3);
         } else if constexpr (G == 2) {
-            pair(acc + 0, H.h02, std::integral_constant<int, 0>{});
-            pair(acc + 8, H.h12, std::integral_constant<int, 1>{});
-#pragma unroll
-            for (int w = 0; w < 8; w++) H.h23[w] = acc[24 + w];
+            pair(acc + 0, H.r[1], std::integral_constant<int, 0>{});  // U[2][z0]
+            pair(acc + 8, H.r[0], std::integral_constant<int, 1>{});  // U[2][z1]
+            keep(1, 3);
         } else {
-            pair(acc + 0, H.h03, std::integral_constant<int, 0>{});
-            pair(acc + 8, H.h13, std::integral_constant<int, 1>{});
-            pair(acc + 16, H.h23, std::integral_constant<int, 2>{});
+            pair(acc + 0, H.r[2], std::integral_constant<int, 0>{});   // U[3][z0]
+            pair(acc + 8, H.r[3], std::integral_constant<int, 1>{});   // U[3][z1]
+            pair(acc + 16, H.r[1], std::integral_constant<int, 2>{});  // U[3][z2]
         }
     }
 };
 
-template <int KD, int M, int PARTS>
-__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode(BsArgs a) {
-    using Kn = Bs6Kernel<KD, M, PARTS>;
+template <int KD, int M, int PARTS, bool EARLY>
+__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY>::BLOCK)) void k_bs6_encode(BsArgs a) {
+    using Kn = Bs6Kernel<KD, M, PARTS, EARLY>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int c = int(threadIdx.x) >> Kn::PB, part = int(threadIdx.x) & (PARTS - 1);
@@ -397,8 +512,8 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode
     auto tile_b0 = [&](int k) { return (xcd * a.tiles_per_xcd + slot + uint32_t(k) * a.nslots) * uint32_t(Kn::W); };
     // counted waits: T = VMEM instructions issued so far by this wave; mk[j] = T right
     // after the DMA of slot (s + j) was issued (j = 0 .. AHEAD-1)
-    int Tn = 0, mk[4] = {0, 0, 0, 0};
-    static_assert(Kn::AHEAD >= 1 && Kn::AHEAD <= 4, "mark shift register has 4 entries");
+    int Tn = 0, mk[5] = {0, 0, 0, 0, 0};
+    static_assert(Kn::AHEAD >= 1 && Kn::AHEAD <= 5, "mark shift register has 5 entries");
     auto issue = [&](int s) {
         if (s < nsteps) {
             const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
@@ -412,7 +527,11 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode
     for (int s = 0; s < Kn::AHEAD; s++) issue(s);
     uint32_t acc[Kn::Q * 8];
     typename Kn::Hold H;
+    const typename Kn::LaneC L = Kn::lane_consts(c, part);
     const uint32_t sc = uint32_t(a.sc);
+#ifdef CLAY_STAMPS
+    uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#endif
     for (int s = 0; s < nsteps; s++) {
         const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
         const uint32_t b0 = tile_b0(k);
@@ -424,11 +543,41 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode
         } else {
             wait_vm_rt(Tn - mk[0]);
         }
+        CLAY_ST(0);
         lds_barrier();
-        issue(s + Kn::AHEAD);  // refills the slot every wave finished reading last step
-        if (y == 0) Kn::template section<0>(slotp, c, part, acc);
-        else if (y == 1) Kn::template section<1>(slotp, c, part, acc);
-        else Kn::template section<2>(slotp, c, part, acc);
+        CLAY_ST(1);
+        if constexpr (EARLY) {
+            uint32_t u[Kn::Q][8];
+            if (y == 0) Kn::template load_prt_all<0>(slotp, L, u);
+            else if (y == 1) Kn::template load_prt_all<1>(slotp, L, u);
+            else Kn::template load_prt_all<2>(slotp, L, u);
+            lds_barrier();         // every wave holds its step in registers: the slot is free
+            issue(s + Kn::AHEAD);  // refill it with the slot AHEAD steps on
+            if (y == 0) Kn::template fold_all<0>(u, acc);
+            else if (y == 1) Kn::template fold_all<1>(u, acc);
+            else Kn::template fold_all<2>(u, acc);
+        } else {
+            // refill the slot every wave finished reading last step, one node per x below
+            const int s2 = s + Kn::AHEAD;
+            const bool more = s2 < nsteps;
+            const int k2 = s2 / Kn::STEPS, r2 = s2 % Kn::STEPS, g2 = r2 / 3, y2 = r2 % 3;
+            const uint32_t nb0 = tile_b0(k2), slot2 = lds0 + uint32_t((s2 % Kn::RING) * Kn::SLOT);
+            uint32_t vl = Kn::MP::inv_d(uint32_t(lane));
+            asm volatile("" : "+v"(vl));
+            auto pre = [&](auto xc) BS_INL {
+                constexpr int x = decltype(xc)::value;
+                if (more) Kn::template dma_node_any<x>(y2, a, slot2, wave, vl, nb0, g2);
+            };
+            CLAY_ST(2);
+            if (y == 0) Kn::template section<0>(slotp, L, acc, pre);
+            else if (y == 1) Kn::template section<1>(slotp, L, acc, pre);
+            else Kn::template section<2>(slotp, L, acc, pre);
+            if (more) Tn += Kn::ndma(y2);
+#pragma unroll
+            for (int j = 0; j + 1 < Kn::AHEAD; j++) mk[j] = mk[j + 1];
+            mk[Kn::AHEAD - 1] = Tn;
+        }
+        CLAY_ST(3);
         if (y == 2) {
             const uint32_t pos = b0 + uint32_t(32 * part);
             const int nv = pos >= sc ? 0 : ((sc - pos) / 8 > 4 ? 4 : int((sc - pos) / 8));
@@ -438,8 +587,17 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode
             else Kn::template end_group<3>(a, acc, H, c, pos, ragged, nv);
             Tn += Kn::stores(g);
         }
+        CLAY_ST(4);
     }
     wait_vm0();
+#ifdef CLAY_STAMPS
+    CLAY_ST(5);
+    if (lane == 0) {
+        uint64_t *o = g_clay_stamps + (uint64_t(blockIdx.x) * Kn::WAVES + wave) * 8;
+        for (int i = 0; i < 6; i++) o[i] = st_acc[i];
+        o[6] = uint64_t(nsteps);
+    }
+#endif
 }
 
 }  // namespace bs

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Device-resident timing of every SURVEY.md §8 configuration on one GPU (inputs resident in
+HBM, HIP events on the launch stream, median of N runs).  Algorithmic bytes per SURVEY §8(d):
+encode  read k*chunk + write m*chunk
+decode  read (n-e)*chunk + write (#erased data nodes)*chunk
+repair  read d*beta*sc + write chunk
+Prints one JSON object per configuration."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import clay_amd  # noqa: E402
+from clay_amd import ClayCode  # noqa: E402
+
+RUNS = int(os.environ.get("RUNS", "10"))
+stream = torch.cuda.current_stream()
+
+
+def timed(fn):
+    ts = []
+    for i in range(RUNS + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if i >= 2:
+            ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts)), float(np.min(ts))
+
+
+def report(name, ms, mn, algo, extra=None):
+    d = {"config": name, "median_ms": round(ms, 4), "min_ms": round(mn, 4),
+         "algorithmic_bytes": int(algo), "GBps": round(algo / (ms * 1e-3) / 1e9, 1),
+         "frac_of_8TBps": round(algo / (ms * 1e-3) / 8e12, 4), "path": clay_amd.last_encode_path(),
+         "launches": clay_amd.last_launch_count()}
+    if extra:
+        d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def rnd(n, chunk, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (n, chunk), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def encode_cfg(k, m, d, stripe):
+    c = ClayCode(k, m, d)
+    chunk = c.encoded_chunk_size(stripe)
+    data, par = rnd(k, chunk, 1), torch.empty((m, chunk), dtype=torch.uint8, device="cuda")
+    ms, mn = timed(lambda: c.encode_device([data[i] for i in range(k)], [par[i] for i in range(m)], chunk, 0,
+                                           stream.cuda_stream))
+    report(f"encode ({k},{m},{d}) {stripe >> 20} MiB", ms, mn, (k + m) * chunk)
+
+
+def decode_cfg(k, m, d, stripe, er):
+    c = ClayCode(k, m, d)
+    chunk = c.encoded_chunk_size(stripe)
+    full = rnd(c.n, chunk, 2)
+    outs = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
+    ins = [None if i in er else full[i] for i in range(c.n)]
+    ous = [outs[i] if i in er else None for i in range(c.n)]
+    ms, mn = timed(lambda: c.decode_device(ins, er, ous, chunk, 0, stream.cuda_stream))
+    ndata = sum(1 for e in er if e < k)
+    report(f"decode ({k},{m},{d}) {stripe >> 20} MiB erasures {er}", ms, mn,
+           (c.n - len(er)) * chunk + ndata * chunk, {"writes_counted": "erased data nodes only"})
+
+
+def repair_cfg(k, m, d, chunk, lost):
+    c = ClayCode(k, m, d)
+    sc = chunk // c.sub_chunk_no
+    info = c.minimum_to_repair(lost, [i for i in range(c.n) if i != lost])
+    helpers = [h for h, _ in info]
+    beta = len(info[0][1])
+    hb = rnd(len(helpers), beta * sc, 3)
+    out = torch.empty(chunk, dtype=torch.uint8, device="cuda")
+    ms, mn = timed(lambda: c.repair_device(lost, helpers, [hb[i] for i in range(len(helpers))], chunk, out, 0,
+                                           stream.cuda_stream))
+    report(f"repair ({k},{m},{d}) chunk {chunk} node {lost}", ms, mn, len(helpers) * beta * sc + chunk)
+
+
+if __name__ == "__main__":
+    encode_cfg(10, 4, 13, 1 << 30)
+    encode_cfg(4, 2, 5, 64 << 20)
+    decode_cfg(4, 2, 5, 64 << 20, [0])
+    decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])
+    decode_cfg(10, 4, 13, 1 << 30, [0])
+    repair_cfg(9, 3, 11, 268_435_458, 0)
+    repair_cfg(9, 3, 11, 268_435_458, 11)
+    repair_cfg(10, 4, 13, 107_374_592, 0)
