@@ -29,6 +29,7 @@
 #include "gf256.hpp"
 #include "bitslice.hpp"
 #include "bitslice6.hpp"
+#include "bitslice7.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -695,6 +696,48 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     return Error{};
 }
 
+template <bool NT, int PROBE = 0>
+static Error launch_bs7(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
+                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::Bs7Kernel<NT>;
+    using S = typename Kn::K6::S;
+    const clay_code_t &c = cs.code;
+    if (c.k != 10 || c.m != 4 || c.d != 13) return Error{};
+    // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 16
+    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 16) return Error{};
+    for (int p = 0; p < 4; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    static bool attr[64] = {};
+    int dev = 0;
+    CLAY_HIP(hipGetDevice(&dev));
+    if (!attr[dev]) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs7_encode<NT, PROBE>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
+        attr[dev] = true;
+    }
+    // XCD region: sc / 8 rounded up to 32 bytes; one 160 KiB workgroup per CU
+    const uint32_t region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
+    const uint32_t per_xcd = uint32_t(std::max(1, prop.multiProcessorCount / 8));
+    const uint32_t nslots = std::min(per_xcd, std::max(1u, (region + 255u) / 256u));
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::BsArgs a{};
+        for (int i = 0; i < S::K; i++) a.data[i] = i < 10 ? data[s * 10 + i] : nullptr;
+        for (int x = 0; x < 4; x++) a.par[x] = par[s * 4 + x];
+        a.sc = sc;
+        a.tiles_per_xcd = region;
+        a.nslots = nslots;
+        a.ntiles = 0;
+        bs::k_bs7_encode<NT, PROBE><<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        CLAY_HIP(hipGetLastError());
+        t_last_launches++;
+    }
+    t_last_path = NT ? "bitsliced7-k10m4-w256-nt" : "bitsliced7-k10m4-w256";
+    *done = true;
+    return Error{};
+}
+
 template <int KD, int M>
 static Error launch_bs3(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
                         size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
@@ -753,6 +796,20 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     CLAY_HIP(hipGetDeviceProperties(&prop, dev));
     Error e;
     const int key = int(c.k * 100 + c.m);
+    // v7 (v6 compute, per-node LDS map with two steps in flight, balanced tail); tile
+    // override 1 = non-temporal DMA loads
+    if (g_encode_mode == 9) {
+        if (key == 1004) {
+            // override bits: 1 = nt loads; 2 / 4 = memory-only / compute-only probes
+            switch (g_bs_pg) {
+            case 1: e = launch_bs7<true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            case 2: e = launch_bs7<false, 1>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            case 4: e = launch_bs7<false, 2>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            default: e = launch_bs7<false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            }
+        }
+        if (e || *done || g_encode_mode == 9) return e;
+    }
     // v6 (column-per-lane, PFT without exchange): 256-byte tiles / 2-slot ring by default
     // (auto's first choice for (10,4,13)); tile override 4 = 128-byte tiles / 5-slot ring
     if (g_encode_mode == 8 || (g_encode_mode == 0 && g_bs_pg == 0)) {

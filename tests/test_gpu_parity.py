@@ -88,7 +88,8 @@ def test_bitsliced23_encode_matches_oracle(oracle_mod, cfg, scale, variant):
     assert np.array_equal(got, ref), (cfg, scale)
 
 
-@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6", "bitsliced6:4", "bitsliced6:20", "bitsliced6:24"])
+@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6", "bitsliced6:4", "bitsliced6:20", "bitsliced6:24",
+                                     "bitsliced7", "bitsliced7:1"])
 @pytest.mark.parametrize("sc", [64, 72, 104, 128, 1064, 6440, 64 * 300 + 40, 64 * 2000 + 8])
 def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
     """v4 (16-byte LDS-DMA, swizzled stage / accumulator) and v5 (register
@@ -275,6 +276,7 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
     # every encode kernel at the BASELINE size (sc = 419,432: ragged last tile, 8-byte
     # aligned sub-chunks), auto first
     for path, tile, prefix in [("auto", 0, "bitsliced6-k10m4-w256"), ("bitsliced6", 4, "bitsliced6-k10m4-w128"),
+                               ("bitsliced7", 0, "bitsliced7"), ("bitsliced7", 1, "bitsliced7-k10m4-w256-nt"),
                                ("bitsliced4", 0, "bitsliced4"), ("bitsliced2", 0, "bitsliced2"),
                                ("fused", 0, "fused")]:
         par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
