@@ -91,7 +91,7 @@ def _ptr(x) -> int:
 def set_encode_path(mode: str, tile: int = 0) -> str:
     """'auto' | 'staged' | 'fused' | 'bitsliced' | 'bitsliced2' -- process-wide encode path selection
     (`tile` overrides the bit-sliced tile width in 32-byte lanes; 0 = default)."""
-    modes = {"auto": 0, "staged": 1, "fused": 2, "bitsliced": 3, "bitsliced2": 4, "bitsliced3": 5, "bitsliced4": 6, "bitsliced5": 7, "bitsliced6": 8, "bitsliced7": 9}
+    modes = {"auto": 0, "staged": 1, "fused": 2, "bitsliced": 3, "bitsliced2": 4, "bitsliced3": 5, "bitsliced4": 6, "bitsliced5": 7, "bitsliced6": 8, "bitsliced7": 9, "bitsliced8": 10}
     prev = _lib.lib().clay_set_encode_path(modes[mode] | (int(tile) << 8))
     return {v: k for k, v in modes.items()}.get(prev, "auto")
 

@@ -976,7 +976,7 @@ __device__ __forceinline__ void dma16(uint32_t lds_addr, const uint8_t *sbase, u
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     const u32x4 v = {a, b, c, d};
-    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 template <int KD, int M>

@@ -183,7 +183,9 @@ __device__ uint64_t *g_clay_stamps;  // [block][wave][phase] cycle sums (tools/s
 __device__ __forceinline__ void st16s(const uint8_t *sbase, uint32_t voff, uint32_t a, uint32_t b, uint32_t c,
                                       uint32_t d) {
     const u32x4 v = {a, b, c, d};
-    asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
+    // s_nop 1: hipcc does not pad an asm store's data hazard (the next instruction may
+    // overwrite the data VGPRs before the store has read them)
+    asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field)

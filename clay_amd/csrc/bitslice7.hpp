@@ -153,8 +153,8 @@ struct Bs7Kernel {
 
 // a.tiles_per_xcd carries the XCD region length in bytes (multiple of 32), a.nslots the
 // workgroups per XCD; grid = 8 * nslots, one 512-lane workgroup per CU (160 KiB LDS).
-// PROBE (measurement only, wrong bytes): 1 = DMA + stores without the compute,
-// 2 = compute + stores without the DMA
+// PROBE (measurement only, wrong bytes), bits: 1 = no compute, 2 = no DMA, 4 = no parity
+// stores, 8 = no workgroup barriers
 template <bool NT, int PROBE = 0>
 __global__ __launch_bounds__(512) void k_bs7_encode(BsArgs a) {
     using Kn = Bs7Kernel<NT>;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(512) void k_bs7_encode(BsArgs a) {
         mk[Kn::AHEAD - 1] = Tn;
     };
     for (int s = 0; s < Kn::AHEAD; s++) {  // nsteps >= 12
-        if (PROBE == 2) break;
+        if (PROBE & 2) break;
         Kn::dma_step(s % 3, a, lds0, wave, vl0, tm.tile(0, slot, ns), s / 3);
         Tn += Kn::ndma(s % 3);
         push();
@@ -190,18 +190,18 @@ __global__ __launch_bounds__(512) void k_bs7_encode(BsArgs a) {
         const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
         const Tile7 t = tm.tile(k, slot, ns);
         const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
-        if (PROBE == 2) {
+        if (PROBE & 2) {
         } else if (ragged) {  // partial tile (a workgroup's last): drain, patch the straddlers
             wait_vm_n<0>();
             if ((t.vend - t.b0) & 15u) Kn::patch_any(y, a, smem, wave, lane, t, g);
         } else {
             wait_vm_rt(Tn - mk[0]);
         }
-        lds_barrier();
+        if constexpr ((PROBE & 8) == 0) lds_barrier();
         // refill region y - 1 (read by step s - 1; the barrier proved every wave is done)
         // with step s + 2, one node ahead of each node's compute below
         const int s2 = s + Kn::AHEAD;
-        const bool more = s2 < nsteps && PROBE != 2;
+        const bool more = s2 < nsteps && !(PROBE & 2);
         const int k2 = s2 / Kn::STEPS, r2 = s2 % Kn::STEPS, g2 = r2 / 3, y2 = r2 % 3;
         const Tile7 t2 = tm.tile(k2, slot, ns);
         uint32_t vl = vl0;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(512) void k_bs7_encode(BsArgs a) {
             constexpr int x = decltype(xc)::value;
             if (more) Kn::template dma_node_any<x>(y2, a, lds0, wave, vl, t2, g2);
         };
-        if constexpr (PROBE == 1) {
+        if constexpr ((PROBE & 1) != 0) {
             sfor<Kn::Q>([&](auto xc) BS_INL { pre(xc); });
             if (y == 0 && g == 0)
 #pragma unroll
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(512) void k_bs7_encode(BsArgs a) {
         }
         if (more) Tn += Kn::ndma(y2);
         push();
-        if (y == 2) {
+        if (y == 2 && !(PROBE & 4)) {
             const uint32_t pos = t.b0 + uint32_t(32 * part);
             const int nv = pos >= t.vend ? 0 : ((t.vend - pos) / 8 > 4 ? 4 : int((t.vend - pos) / 8));
             if (g == 0) K6::template end_group<0>(a, acc, H, c, pos, ragged, nv);

@@ -30,6 +30,7 @@
 #include "bitslice.hpp"
 #include "bitslice6.hpp"
 #include "bitslice7.hpp"
+#include "bitslice8.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -738,6 +739,47 @@ static Error launch_bs7(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     return Error{};
 }
 
+static Error launch_bs8(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
+                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::Bs8Kernel;
+    using S = typename Kn::S;
+    const clay_code_t &c = cs.code;
+    if (c.k != 10 || c.m != 4 || c.d != 13) return Error{};
+    // per-lane offsets are 32-bit chunk offsets
+    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 16) return Error{};
+    for (int p = 0; p < 4; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    static bool attr[64] = {};
+    int dev = 0;
+    CLAY_HIP(hipGetDevice(&dev));
+    if (!attr[dev]) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs8_encode),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
+        attr[dev] = true;
+    }
+    // XCD region: sc / 8 rounded up to 32 bytes (TileMap7); one workgroup per CU
+    const uint32_t region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
+    const uint32_t per_xcd = uint32_t(std::max(1, prop.multiProcessorCount / 8));
+    const uint32_t nslots = std::min(per_xcd, std::max(1u, (region + 255u) / 256u));
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::BsArgs a{};
+        for (int i = 0; i < S::K; i++) a.data[i] = i < 10 ? data[s * 10 + i] : nullptr;
+        for (int x = 0; x < 4; x++) a.par[x] = par[s * 4 + x];
+        a.sc = sc;
+        a.tiles_per_xcd = region;
+        a.nslots = nslots;
+        a.ntiles = 0;
+        bs::k_bs8_encode<<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        CLAY_HIP(hipGetLastError());
+        t_last_launches++;
+    }
+    t_last_path = "bitsliced8-k10m4-w256";
+    *done = true;
+    return Error{};
+}
+
 template <int KD, int M>
 static Error launch_bs3(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
                         size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
@@ -796,15 +838,24 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     CLAY_HIP(hipGetDeviceProperties(&prop, dev));
     Error e;
     const int key = int(c.k * 100 + c.m);
+    // v8 (register-staged loads three steps deep, plane exchange through LDS)
+    if (g_encode_mode == 10) {
+        if (key == 1004) e = launch_bs8(cs, prop, data, par, n_stripes, sc, stream, done);
+        if (e || *done || g_encode_mode == 10) return e;
+    }
     // v7 (v6 compute, per-node LDS map with two steps in flight, balanced tail); tile
     // override 1 = non-temporal DMA loads
     if (g_encode_mode == 9) {
         if (key == 1004) {
-            // override bits: 1 = nt loads; 2 / 4 = memory-only / compute-only probes
+            // override: 1 = nt loads; probes (wrong bytes): 2 memory-only, 4 compute-only,
+            // 6 reads-only, 10 memory-only without barriers, 14 reads-only without barriers
             switch (g_bs_pg) {
             case 1: e = launch_bs7<true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             case 2: e = launch_bs7<false, 1>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             case 4: e = launch_bs7<false, 2>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            case 6: e = launch_bs7<false, 5>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            case 10: e = launch_bs7<false, 9>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            case 14: e = launch_bs7<false, 13>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             default: e = launch_bs7<false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             }
         }
