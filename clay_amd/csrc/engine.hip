@@ -78,6 +78,57 @@ __global__ __launch_bounds__(kExecBlock) void k_exec(ExecPtrs P, const DevOp *__
     vstore<VW>(P.p[op.base] + uint64_t(op.slot) * sc + pos, acc);
 }
 
+// Grouped staged executor: one workgroup = one source-sharing op group x one tile.
+// Each source tile is loaded once, split into its perm-table indices once, and
+// multiplied into up to MAXD destination accumulators (dst_d = XOR_s coef[d][s] * src_s).
+template <int VW, int MAXD>
+__global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup *__restrict__ groups,
+                                                      const DevSrc *__restrict__ gsrcs,
+                                                      const DevSrc *__restrict__ gdsts,
+                                                      const uint32_t *__restrict__ gcoef,
+                                                      const uint32_t *__restrict__ tabs, uint32_t g0,
+                                                      uint32_t tiles, uint64_t sc) {
+    constexpr int NW = (VW + 3) / 4;
+    const uint32_t gi = blockIdx.x / tiles, tile = blockIdx.x - gi * tiles;
+    const DevGroup g = groups[g0 + gi];
+    const uint64_t pos = (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
+    if (pos >= sc) return;
+    uint32_t acc[MAXD][NW];
+#pragma unroll
+    for (int d = 0; d < MAXD; d++)
+#pragma unroll
+        for (int w = 0; w < NW; w++) acc[d][w] = 0;
+    for (uint32_t s = 0; s < g.nsrc; ++s) {
+        const DevSrc src = gsrcs[g.src_begin + s];
+        const Words<NW> v = vload<VW>(P.p[src.base] + uint64_t(src.slot) * sc + pos);
+        GfIdx ix[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) ix[w] = gf_idx(v.w[w]);
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) {
+            if (d >= int(g.ndst)) break;
+            const uint32_t c = gcoef[g.coef_begin + d * g.nsrc + s];
+            if (c == 1) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) acc[d][w] ^= v.w[w];
+            } else {
+                const GfTab t = load_tab(tabs + c * 8);
+#pragma unroll
+                for (int w = 0; w < NW; w++) acc[d][w] ^= gf_mul_idx(ix[w], t);
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) {
+        if (d >= int(g.ndst)) break;
+        const DevSrc dst = gdsts[g.dst_begin + d];
+        Words<NW> o;
+#pragma unroll
+        for (int w = 0; w < NW; w++) o.w[w] = acc[d][w];
+        vstore<VW>(P.p[dst.base] + uint64_t(dst.slot) * sc + pos, o);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Fused encode (parity = last y-section).  See file header and DESIGN.md.
 // LDS: acc[p][z][W] bytes (p < Q parity rows, z < alpha layers, W positions).
@@ -264,6 +315,12 @@ struct CodeState {
     std::unique_ptr<Plan> enc;
     std::map<std::vector<uint8_t>, std::unique_ptr<Plan>> dec, rep;
     std::map<std::pair<const Plan *, int>, std::pair<void *, void *>> dplan;
+    struct DevGrouped {
+        const DevGroup *groups;
+        const DevSrc *srcs, *dsts;
+        const uint32_t *coef;
+    };
+    std::map<std::pair<const Plan *, int>, DevGrouped> gplan;
     std::map<int, uint32_t *> mtab;
     explicit CodeState(const clay_code_t &c) : code(c), rs(c) {}
 };
@@ -338,6 +395,56 @@ static Error upload_plan(CodeState &cs, const Plan &pl, int dev, const DevOp **o
     return Error{};
 }
 
+template <typename T>
+static Error upload_vec(const std::vector<T> &v, const T **out) {
+    void *p = nullptr;
+    CLAY_HIP(hipMalloc(&p, std::max<size_t>(1, v.size()) * sizeof(T)));
+    if (!v.empty()) CLAY_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = static_cast<const T *>(p);
+    return Error{};
+}
+
+static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::DevGrouped *out) {
+    auto key = std::make_pair(&pl, dev);
+    auto it = cs.gplan.find(key);
+    if (it == cs.gplan.end()) {
+        CodeState::DevGrouped g{};
+        Error e = upload_vec(pl.groups, &g.groups);
+        if (!e) e = upload_vec(pl.gsrcs, &g.srcs);
+        if (!e) e = upload_vec(pl.gdsts, &g.dsts);
+        if (!e) e = upload_vec(pl.gcoef, &g.coef);
+        if (e) return e;
+        it = cs.gplan.emplace(key, g).first;
+    }
+    *out = it->second;
+    return Error{};
+}
+
+// CLAY_EXEC=ops selects the one-op-per-block executor (k_exec) for A/B runs.
+static bool exec_grouped() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("CLAY_EXEC");
+        v = (e && std::strcmp(e, "ops") == 0) ? 0 : 1;
+    }
+    return v == 1;
+}
+
+template <int VW>
+static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
+                         const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
+                         uint64_t sc) {
+    dim3 block(kExecBlock);
+    if (maxd <= 1)
+        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+    else if (maxd <= 2)
+        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+    else if (maxd <= 4)
+        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+    else
+        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+}
+
 static Error ensure_ws(DevState &ds, void *stream, size_t bytes, void **out) {
     Workspace &w = ds.ws[stream];
     if (w.bytes < bytes) {
@@ -380,6 +487,31 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     const uint64_t per_thread = uint64_t(vw);
     const uint32_t tiles = uint32_t((sc / per_thread + kExecBlock - 1) / kExecBlock);
     size_t launches = 0;
+    if (exec_grouped() && pl.gstage_begin.size() == pl.stage_begin.size()) {
+        CodeState::DevGrouped g{};
+        e = upload_groups(cs, pl, dev, &g);
+        if (e) return e;
+        for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
+            uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
+            const uint32_t maxd = pl.gstage_maxd[s];
+            while (b < end) {
+                uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
+                dim3 grid(n * tiles);
+                switch (vw) {
+                case 16: launch_gexec<16>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
+                case 8: launch_gexec<8>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
+                case 4: launch_gexec<4>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
+                case 2: launch_gexec<2>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
+                default: launch_gexec<1>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
+                }
+                CLAY_HIP(hipGetLastError());
+                launches++;
+                b += n;
+            }
+        }
+        t_last_launches += launches;
+        return Error{};
+    }
     for (size_t s = 0; s + 1 < pl.stage_begin.size(); s++) {
         uint32_t b = pl.stage_begin[s], end = pl.stage_begin[s + 1];
         while (b < end) {

@@ -2,6 +2,9 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <map>
+
+#include <algorithm>
 #include <string>
 
 #include "gf256.hpp"
@@ -128,7 +131,74 @@ std::unique_ptr<Plan> PlanBuilder::finalize(const std::vector<uint64_t> &outputs
         }
         plan->stage_begin.push_back(uint32_t(plan->ops.size()));
     }
+    plan->group_ops();
     return plan;
+}
+
+// Merge the ops of each stage that read the same (base, slot) source set.  Ops of
+// one stage never read each other's destinations (levels above), so a group may
+// read all of its sources before writing any destination.
+void Plan::group_ops() {
+    groups.clear(); gsrcs.clear(); gdsts.clear(); gcoef.clear(); gstage_begin.assign(1, 0); gstage_maxd.clear();
+    struct G {
+        std::vector<std::pair<uint32_t, uint32_t>> src;  // sorted (base, slot)
+        std::vector<DevSrc> dst;
+        std::vector<std::vector<uint32_t>> coef;          // per dst, aligned with src
+    };
+    for (size_t s = 0; s + 1 < stage_begin.size(); s++) {
+        std::vector<G> gs;
+        std::map<std::vector<std::pair<uint32_t, uint32_t>>, size_t> open;
+        for (uint32_t i = stage_begin[s]; i < stage_begin[s + 1]; i++) {
+            const DevOp &op = ops[i];
+            std::vector<std::pair<std::pair<uint32_t, uint32_t>, uint32_t>> t;
+            for (uint32_t j = 0; j < op.nsrc; j++) {
+                const DevSrc &d = srcs[op.src_begin + j];
+                t.push_back({{d.base, d.slot}, d.coef});
+            }
+            std::sort(t.begin(), t.end());
+            bool dup = false;  // a repeated source term stays a single-op group (coefs not merged)
+            for (size_t j = 1; j < t.size(); j++) dup |= t[j].first == t[j - 1].first;
+            std::vector<std::pair<uint32_t, uint32_t>> key;
+            for (auto &x : t) key.push_back(x.first);
+            size_t gi;
+            auto it = dup || key.empty() ? open.end() : open.find(key);
+            if (it != open.end() && gs[it->second].dst.size() < kMaxGroupDst) {
+                gi = it->second;
+            } else {
+                gi = gs.size();
+                gs.push_back(G{key, {}, {}});
+                if (!dup && !key.empty()) open[key] = gi;
+            }
+            DevSrc dd{};
+            dd.base = op.base;
+            dd.slot = op.slot;
+            gs[gi].dst.push_back(dd);
+            std::vector<uint32_t> cf;
+            for (auto &x : t) cf.push_back(x.second);
+            gs[gi].coef.push_back(cf);
+        }
+        uint32_t maxd = 1;
+        for (auto &g : gs) {
+            DevGroup dg{};
+            dg.src_begin = uint32_t(gsrcs.size());
+            dg.nsrc = uint32_t(g.src.size());
+            dg.dst_begin = uint32_t(gdsts.size());
+            dg.ndst = uint32_t(g.dst.size());
+            dg.coef_begin = uint32_t(gcoef.size());
+            for (auto &x : g.src) {
+                DevSrc d{};
+                d.base = x.first;
+                d.slot = x.second;
+                gsrcs.push_back(d);
+            }
+            for (auto &d : g.dst) gdsts.push_back(d);
+            for (auto &cf : g.coef) gcoef.insert(gcoef.end(), cf.begin(), cf.end());
+            maxd = std::max(maxd, dg.ndst);
+            groups.push_back(dg);
+        }
+        gstage_begin.push_back(uint32_t(groups.size()));
+        gstage_maxd.push_back(maxd);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -42,6 +42,19 @@ struct DevOp {
     uint32_t src_begin, nsrc;  // into DevSrc array
 };
 
+// Multi-destination group (one launch block = one group x one tile): every op of
+// a stage that reads exactly the same source set -- the m parity/reconstruct rows
+// of one layer's RS call (decode.rs:369-398), the two halves of a PRT/PFT pair
+// (transforms.rs:42-125) -- is merged, so each source tile is read from HBM once
+// and feeds up to kMaxGroupDst accumulators.
+constexpr uint32_t kMaxGroupDst = 8;
+struct DevGroup {
+    uint32_t src_begin, nsrc;  // into gsrcs (coef field unused)
+    uint32_t dst_begin, ndst;  // into gdsts
+    uint32_t coef_begin;       // gcoef[coef_begin + d*nsrc + s]
+    uint32_t pad[3];
+};
+
 struct Plan {
     // pointer table layout: [0, tn) = C[node], [tn, 2tn) = H[node], 2tn = U workspace
     // (slot = node*alpha + z), 2tn+1 = OUT.
@@ -49,10 +62,17 @@ struct Plan {
     std::vector<DevOp> ops;           // grouped by stage
     std::vector<DevSrc> srcs;
     std::vector<uint32_t> stage_begin;  // size = stages + 1
+    // grouped form of the same stages (built by group_ops(); what the device runs)
+    std::vector<DevGroup> groups;
+    std::vector<DevSrc> gsrcs, gdsts;
+    std::vector<uint32_t> gcoef;
+    std::vector<uint32_t> gstage_begin;  // size = stages + 1, into groups
+    std::vector<uint32_t> gstage_maxd;   // max ndst per stage
     bool uses_u = false;
     size_t total_src_terms = 0;
     // device copies (owned by the runtime, per device)
     void *d_ops = nullptr, *d_srcs = nullptr;
+    void group_ops();
     int device = -1;
 };
 
