@@ -93,6 +93,12 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     const DevGroup g = groups[g0 + gi];
     const uint64_t pos = (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
     if (pos >= sc) return;
+    // Regions start at slot*sc, which is only 2-byte aligned for e.g. the (9,3,11)
+    // chunk of 268,435,458 B; gfx950 global loads/stores run in unaligned mode, so
+    // full lanes use 16-byte accesses at any address and only the last lane of a
+    // region (pos + VW > sc) falls back to bytes.
+    const bool full = pos + VW <= sc;
+    const uint32_t nb = full ? uint32_t(VW) : uint32_t(sc - pos);
     uint32_t acc[MAXD][NW];
 #pragma unroll
     for (int d = 0; d < MAXD; d++)
@@ -100,7 +106,15 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
         for (int w = 0; w < NW; w++) acc[d][w] = 0;
     for (uint32_t s = 0; s < g.nsrc; ++s) {
         const DevSrc src = gsrcs[g.src_begin + s];
-        const Words<NW> v = vload<VW>(P.p[src.base] + uint64_t(src.slot) * sc + pos);
+        const uint8_t *sp = P.p[src.base] + uint64_t(src.slot) * sc + pos;
+        Words<NW> v;
+        if (full) {
+            __builtin_memcpy(&v, sp, sizeof(v));
+        } else {
+            uint8_t tb[NW * 4] = {};
+            for (uint32_t i = 0; i < nb; i++) tb[i] = sp[i];
+            __builtin_memcpy(&v, tb, sizeof(v));
+        }
         GfIdx ix[NW];
 #pragma unroll
         for (int w = 0; w < NW; w++) ix[w] = gf_idx(v.w[w]);
@@ -122,10 +136,14 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     for (int d = 0; d < MAXD; d++) {
         if (d >= int(g.ndst)) break;
         const DevSrc dst = gdsts[g.dst_begin + d];
-        Words<NW> o;
-#pragma unroll
-        for (int w = 0; w < NW; w++) o.w[w] = acc[d][w];
-        vstore<VW>(P.p[dst.base] + uint64_t(dst.slot) * sc + pos, o);
+        uint8_t *dp = P.p[dst.base] + uint64_t(dst.slot) * sc + pos;
+        if (full) {
+            __builtin_memcpy(dp, acc[d], sizeof(acc[d]));
+        } else {
+            uint8_t tb[NW * 4];
+            __builtin_memcpy(tb, acc[d], sizeof(tb));
+            for (uint32_t i = 0; i < nb; i++) dp[i] = tb[i];
+        }
     }
 }
 
@@ -488,6 +506,9 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     const uint32_t tiles = uint32_t((sc / per_thread + kExecBlock - 1) / kExecBlock);
     size_t launches = 0;
     if (exec_grouped() && pl.gstage_begin.size() == pl.stage_begin.size()) {
+        // 16 bytes per lane regardless of sc / pointer alignment (see k_gexec)
+        vw = 16;
+        const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
         CodeState::DevGrouped g{};
         e = upload_groups(cs, pl, dev, &g);
         if (e) return e;

@@ -324,3 +324,24 @@ def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda):
     c.repair_device(lost, [h for h, _ in info], hb, chunk, out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13)])
+@pytest.mark.parametrize("sc", [16 * 257 + 2, 16 * 1000 + 9, 16 * 3001])
+def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc):
+    """Sub-chunks spanning several executor tiles whose regions start at 2-byte / odd
+    offsets (the (9,3,11) 256 MiB chunk has sc = 3,314,018): random (non-codeword)
+    inputs, decode and repair byte-identical to the oracle."""
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc)
+    chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+    er = list(range(0, c.n, c.q))[:m]
+    av = {i: chunks[i] for i in range(c.n) if i not in er}
+    assert c.decode(av, er) == o.decode(av, er), (cfg, sc, er)
+    for lost in (0, c.n - 1):
+        avail = [i for i in range(c.n) if i != lost]
+        info = c.minimum_to_repair(lost, avail)
+        pr = {h: rng.integers(0, 256, len(idx) * sc, dtype=np.uint8) for h, idx in info}
+        assert c.repair(lost, pr, chunk) == o.repair(lost, pr, chunk), (cfg, sc, lost)
