@@ -82,9 +82,11 @@ def _sizes(vals) -> "C.Array":
 
 
 def _ptr(x) -> int:
-    """Device pointer of a torch tensor or a raw int."""
+    """Address of a torch tensor, a numpy array or a raw int."""
     if hasattr(x, "data_ptr"):
         return int(x.data_ptr())
+    if hasattr(x, "__array_interface__"):
+        return int(x.__array_interface__["data"][0])
     return int(x)
 
 
@@ -229,6 +231,20 @@ class ClayCode:
         rc = _lib.lib().clay_encode_device_batch(C.byref(self._c), dp, pp, int(n_stripes),
                                                  int(chunk_size), int(device),
                                                  C.c_void_p(int(stream)), C.byref(err))
+        if rc:
+            _raise(rc, err)
+
+    def encode_host_pipelined(self, data_chunks, parity_chunks, chunk_size: int, device: int = 0,
+                              piece_bytes: int = 0, n_streams: int = 0):
+        """Host-streaming encode (clay.h clay_encode_host_pipelined): k host data buffers in,
+        m host parity buffers out (numpy arrays or CPU tensors; pinned tensors overlap H2D,
+        encode and D2H).  Blocks until the parity is in host memory."""
+        dp = (C.c_void_p * self.k)(*[_ptr(x) for x in data_chunks])
+        pp = (C.c_void_p * self.m)(*[_ptr(x) for x in parity_chunks])
+        err = ClayErrorStruct()
+        rc = _lib.lib().clay_encode_host_pipelined(C.byref(self._c), dp, pp, int(chunk_size),
+                                                   int(device), int(piece_bytes), int(n_streams),
+                                                   C.byref(err))
         if rc:
             _raise(rc, err)
 

@@ -42,6 +42,8 @@ SIGNATURES = {
     "clay_encode_device": (C.c_int, [_code_p, _P(_vp), _P(_vp), _sz, C.c_int, _vp, _err_p]),
     "clay_encode_device_batch": (C.c_int, [_code_p, _P(_vp), _P(_vp), _sz, _sz, C.c_int, _vp,
                                            _err_p]),
+    "clay_encode_host_pipelined": (C.c_int, [_code_p, _P(_vp), _P(_vp), _sz, C.c_int, _sz, C.c_int,
+                                             _err_p]),
     "clay_decode_device": (C.c_int, [_code_p, _P(_vp), _P(_sz), _sz, _P(_vp), _sz, C.c_int, _vp,
                                      _err_p]),
     "clay_repair_device": (C.c_int, [_code_p, _sz, _P(_sz), _P(_vp), _sz, _sz, _vp, C.c_int, _vp,

@@ -324,6 +324,10 @@ struct DevState {
     std::mutex host_mu;                            // serialises the host-buffer API per device
     hipStream_t host_stream = nullptr;
     Workspace host_bufs[3];
+    // host-streaming pipeline (clay_encode_host_pipelined): streams + per-stream piece buffers
+    std::mutex pipe_mu;
+    std::vector<hipStream_t> pipe_streams;
+    std::vector<Workspace> pipe_bufs;
 };
 static DevState g_dev[64];
 
@@ -1388,6 +1392,98 @@ int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, con
         }
         std::copy(p->stage_begin.begin(), p->stage_begin.end(), stages_out);
     }
+    return 0;
+}
+
+// Host-streaming encode.  Each byte offset of the sub-chunks
+// is an independent codeword, so the stripe is cut into pieces of `w` bytes of
+// every sub-chunk.  Piece p of node i is alpha rows of w bytes at pitch sc in
+// host memory -> one hipMemcpy2DAsync into a compact piece buffer (sub-chunk
+// size w), one device encode of that piece, and one 2D copy of each parity piece
+// back.  Pieces round-robin over `ns` streams, so H2D of piece p+1, the encode of
+// piece p and the D2H of piece p-1 overlap (PCIe is full duplex).
+int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *data_chunks,
+                               uint8_t *const *parity_chunks, size_t chunk, int device, size_t piece_bytes,
+                               int n_streams, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = check_code(code);
+    if (e) return report(e, err);
+    const clay_code_t &c = *code;
+    if (!data_chunks || !parity_chunks)
+        return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null chunk array"), err);
+    if (chunk == 0 || chunk % c.sub_chunk_no != 0)
+        return report(make_error(CLAY_ERR_INVALID_CHUNK_SIZE, c.sub_chunk_no, chunk, 0,
+                                 "Invalid chunk size: expected divisible by %zu, got %zu", c.sub_chunk_no, chunk),
+                      err);
+    for (size_t i = 0; i < c.k; i++)
+        if (!data_chunks[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null data chunk"), err);
+    for (size_t i = 0; i < c.m; i++)
+        if (!parity_chunks[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk"), err);
+    const size_t alpha = c.sub_chunk_no, sc = chunk / alpha, K = c.k, M = c.m;
+    size_t w = piece_bytes ? piece_bytes : (size_t(32) << 20) / (K * alpha);
+    w = w >= 256 ? w / 256 * 256 : (w + 7) / 8 * 8;  // whole 256-byte encode tiles (8-byte minimum)
+    w = std::max<size_t>(8, std::min(w, sc));
+    const size_t np = (sc + w - 1) / w;
+    const int ns = int(std::max<size_t>(1, std::min<size_t>(np, n_streams > 0 ? size_t(n_streams) : 3)));
+    DevState *ds;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        e = dev_state(device, &ds);
+    }
+    if (e) return report(e, err);
+    std::lock_guard<std::mutex> pl(ds->pipe_mu);
+    DeviceGuard g(device);
+    auto fail = [&](hipError_t he) {
+        return report(make_error(CLAY_ERR_DEVICE, size_t(he), 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+    };
+    hipError_t he;
+    while (int(ds->pipe_streams.size()) < ns) {
+        hipStream_t st;
+        if ((he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return fail(he);
+        ds->pipe_streams.push_back(st);
+        ds->pipe_bufs.emplace_back();
+    }
+    const size_t need = (K + M) * alpha * w;
+    for (int s = 0; s < ns; s++) {
+        Workspace &b = ds->pipe_bufs[s];
+        if (b.bytes < need) {
+            if (b.ptr) {
+                if ((he = hipStreamSynchronize(ds->pipe_streams[s])) != hipSuccess) return fail(he);
+                if ((he = hipFree(b.ptr)) != hipSuccess) return fail(he);
+                b.ptr = nullptr;
+                b.bytes = 0;
+            }
+            if ((he = hipMalloc(&b.ptr, need)) != hipSuccess) return fail(he);
+            b.bytes = need;
+        }
+    }
+    std::vector<const uint8_t *> dp(K);
+    std::vector<uint8_t *> pp(M);
+    size_t launches = 0;
+    for (size_t p = 0; p < np; p++) {
+        const int s = int(p % size_t(ns));
+        hipStream_t st = ds->pipe_streams[s];
+        uint8_t *buf = static_cast<uint8_t *>(ds->pipe_bufs[s].ptr);
+        const size_t off = p * w, wp = std::min(w, sc - off);
+        for (size_t i = 0; i < K; i++) {
+            uint8_t *dst = buf + i * alpha * wp;
+            if ((he = hipMemcpy2DAsync(dst, wp, data_chunks[i] + off, sc, wp, alpha, hipMemcpyHostToDevice, st)) !=
+                hipSuccess)
+                return fail(he);
+            dp[i] = dst;
+        }
+        for (size_t j = 0; j < M; j++) pp[j] = buf + (K + j) * alpha * wp;
+        e = encode_device_impl(code, dp.data(), pp.data(), 1, alpha * wp, device, st);
+        if (e) return report(e, err);
+        launches += t_last_launches;
+        for (size_t j = 0; j < M; j++)
+            if ((he = hipMemcpy2DAsync(parity_chunks[j] + off, sc, pp[j], wp, wp, alpha, hipMemcpyDeviceToHost, st)) !=
+                hipSuccess)
+                return fail(he);
+    }
+    for (int s = 0; s < ns; s++)
+        if ((he = hipStreamSynchronize(ds->pipe_streams[s])) != hipSuccess) return fail(he);
+    t_last_launches = launches;
     return 0;
 }
 

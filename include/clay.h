@@ -136,6 +136,20 @@ int clay_encode_device_batch(const clay_code_t *code, const uint8_t *const *data
                              uint8_t *const *parity_chunks, size_t n_stripes, size_t chunk_size,
                              int device, void *stream, clay_error_t *err);
 
+/* Host-streaming encode (host memory in, host memory out; blocking).  data_chunks:
+ * k host pointers, parity_chunks: m host pointers (chunk_size bytes each; pin
+ * them, e.g. hipHostMalloc / hipHostRegister, for overlap).  The stripe is cut
+ * into pieces of piece_bytes (0 = auto, ~32 MiB of input per piece) of every
+ * sub-chunk; each piece is copied in with one 2D copy per node, encoded on the
+ * device and its parity copied out, round-robin over n_streams (0 = 3) streams
+ * so H2D, encode and D2H of consecutive pieces overlap.  Same parity bytes as
+ * clay_encode / clay_encode_device.  Replaces the host-side entry of
+ * ClayCode::encode (lib.rs:165-167 -> encode.rs:30-80) for callers that hold
+ * the data chunks in host memory. */
+int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *data_chunks,
+                               uint8_t *const *parity_chunks, size_t chunk_size, int device,
+                               size_t piece_bytes, int n_streams, clay_error_t *err);
+
 /* Decode / rebuild on device.  chunks: n device pointers, NULL for every erased
  * node (validation as decode.rs:36-126 with available = the non-NULL entries).
  * out_chunks: n device pointers; for every erased DATA node out_chunks[i] must
