@@ -2,9 +2,8 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
-
-#include <algorithm>
 #include <string>
 
 #include "gf256.hpp"
@@ -66,7 +65,79 @@ void PlanBuilder::emit(uint64_t dst, const std::vector<std::pair<uint64_t, uint8
     cur[dst] = int32_t(ops.size() - 1);
 }
 
+// Forward substitution of short ops over stable inputs.  An op that is not an
+// output and whose <= 2 sources are input regions nothing ever rewrites (the red
+// copies U = C, decode.rs:284-289, and PRT pairs U = C + g*C*, transforms.rs:42-55,
+// over available chunks / helper payloads) is folded into every consumer:
+// consumer term c*dst becomes c*coef_s*src_s, equal terms merge by XOR.  The
+// linear map is unchanged; the U round trip through HBM disappears and the
+// consumer group reads the inputs directly.  CLAY_PLAN_INLINE=0 disables.
+void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
+    static int enabled = -1;
+    if (enabled < 0) {
+        const char *e = getenv("CLAY_PLAN_INLINE");
+        enabled = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (!enabled) return;
+    const size_t n = ops.size();
+    std::unordered_map<uint64_t, int> written;
+    for (const auto &o : ops) written[o.dst] = 1;
+    std::vector<uint8_t> is_out(n, 0), inl(n, 0);
+    for (uint64_t o : outputs) {
+        auto it = cur.find(o);
+        if (it != cur.end() && it->second >= 0) is_out[it->second] = 1;
+    }
+    // readers counted per consumer layer (dst slot): the RS rows of one layer form one
+    // group on the device and read a shared source once
+    std::vector<std::vector<uint32_t>> rl(n);
+    for (const auto &o : ops)
+        for (const auto &t : o.src)
+            if (t.ver >= 0 && std::find(rl[t.ver].begin(), rl[t.ver].end(), rslot(o.dst)) == rl[t.ver].end())
+                rl[t.ver].push_back(rslot(o.dst));
+    const GF &gf = GF::get();
+    for (size_t i = 0; i < n; i++) {
+        bool any = false;
+        for (const auto &t : ops[i].src) any |= t.ver >= 0 && inl[t.ver];
+        if (any) {
+            std::vector<Term> nt;
+            for (const auto &t : ops[i].src) {
+                if (t.ver >= 0 && inl[t.ver]) {
+                    for (const auto &u : ops[t.ver].src) nt.push_back(Term{u.key, u.ver, gf.mul(t.coef, u.coef)});
+                } else {
+                    nt.push_back(t);
+                }
+            }
+            std::vector<Term> merged;
+            for (const auto &t : nt) {
+                bool hit = false;
+                for (auto &m : merged)
+                    if (m.key == t.key && m.ver == t.ver) {
+                        m.coef ^= t.coef;
+                        hit = true;
+                        break;
+                    }
+                if (!hit) merged.push_back(t);
+            }
+            merged.erase(std::remove_if(merged.begin(), merged.end(), [](const Term &s) { return s.coef == 0; }),
+                         merged.end());
+            ops[i].src = std::move(merged);
+        }
+        if (is_out[i] || ops[i].src.size() > 2) continue;
+        // sources: never-written inputs (any reader count), or final versions of
+        // computed regions when at most 2 ops read this one (folding then never
+        // adds HBM reads: 2 + 1 + r round-trip bytes vs 2r direct).
+        bool inputs = true, finals = true;
+        for (const auto &t : ops[i].src) {
+            inputs &= t.ver < 0 && !written.count(t.key);
+            auto it = cur.find(t.key);
+            finals &= t.ver < 0 ? !written.count(t.key) : (it != cur.end() && it->second == t.ver);
+        }
+        if (inputs || (finals && rl[i].size() <= 2)) inl[i] = 1;
+    }
+}
+
 std::unique_ptr<Plan> PlanBuilder::finalize(const std::vector<uint64_t> &outputs, uint32_t tn, uint32_t alpha) {
+    inline_inputs(outputs);
     const size_t n = ops.size();
     std::vector<uint8_t> live(n, 0);
     for (uint64_t o : outputs) {

@@ -99,6 +99,7 @@ class PlanBuilder {
 
   private:
     bool is_zero(uint64_t key, int32_t ver) const;
+    void inline_inputs(const std::vector<uint64_t> &outputs);
 };
 
 // Per-code RS cache (generator rows + reconstruct matrices by valid-row set).

@@ -85,10 +85,11 @@ def test_plan_repair_random_helpers(oracle_mod, cfg):
 
 
 def test_plan_stage_counts():
-    """Launch counts the staged engine issues: encode of a q==m code is 3 dependent
-    levels (PRT -> RS -> PFT); 4 erasures in 4 y-sections of (10,4,13) need more."""
+    """Launch counts the staged engine issues: encode of a q==m code is PRT -> RS -> PFT,
+    with the PRT pairs over the data chunks folded into the RS rows (plan.cpp
+    inline_inputs), so 2 dependent levels; 4 erasures in 4 y-sections of (10,4,13) need more."""
     c = ClayCode(10, 4, 13)
-    assert len(E.export_plan(c, 0)[2]) - 1 == 3
+    assert len(E.export_plan(c, 0)[2]) - 1 == 2
     mask = [0] * 16
     for i in (0, 4, 8, 14):
         mask[i] = 1
