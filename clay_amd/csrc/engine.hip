@@ -87,18 +87,18 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                                                       const DevSrc *__restrict__ gdsts,
                                                       const uint32_t *__restrict__ gcoef,
                                                       const uint32_t *__restrict__ tabs, uint32_t g0,
-                                                      uint32_t tiles, uint64_t sc) {
+                                                      uint32_t tiles, uint64_t sc, uint64_t r0, uint64_t r1) {
     constexpr int NW = (VW + 3) / 4;
     const uint32_t gi = blockIdx.x / tiles, tile = blockIdx.x - gi * tiles;
     const DevGroup g = groups[g0 + gi];
-    const uint64_t pos = (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
-    if (pos >= sc) return;
+    const uint64_t pos = r0 + (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
+    if (pos >= r1) return;
     // Regions start at slot*sc, which is only 2-byte aligned for e.g. the (9,3,11)
     // chunk of 268,435,458 B; gfx950 global loads/stores run in unaligned mode, so
     // full lanes use 16-byte accesses at any address and only the last lane of a
     // region (pos + VW > sc) falls back to bytes.
-    const bool full = pos + VW <= sc;
-    const uint32_t nb = full ? uint32_t(VW) : uint32_t(sc - pos);
+    const bool full = pos + VW <= r1;
+    const uint32_t nb = full ? uint32_t(VW) : uint32_t(r1 - pos);
     uint32_t acc[MAXD][NW];
 #pragma unroll
     for (int d = 0; d < MAXD; d++)
@@ -455,16 +455,16 @@ static bool exec_grouped() {
 template <int VW>
 static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
-                         uint64_t sc) {
+                         uint64_t sc, uint64_t r0, uint64_t r1) {
     dim3 block(kExecBlock);
     if (maxd <= 1)
-        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
     else if (maxd <= 2)
-        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
     else if (maxd <= 4)
-        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
     else
-        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc);
+        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
 }
 
 static Error ensure_ws(DevState &ds, void *stream, size_t bytes, void **out) {
@@ -510,28 +510,31 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     const uint32_t tiles = uint32_t((sc / per_thread + kExecBlock - 1) / kExecBlock);
     size_t launches = 0;
     if (exec_grouped() && pl.gstage_begin.size() == pl.stage_begin.size()) {
-        // 16 bytes per lane regardless of sc / pointer alignment (see k_gexec)
-        vw = 16;
-        const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+        // 16 bytes per lane regardless of sc / pointer alignment (see k_gexec).
+        // CLAY_EXEC_RANGE=B runs all stages over byte range [r0, r0+B) of every
+        // sub-chunk before the next range (cache-resident U round trips).
+        static const uint64_t range_env = [] {
+            const char *e = getenv("CLAY_EXEC_RANGE");
+            return e ? uint64_t(strtoull(e, nullptr, 10)) / 16 * 16 : uint64_t(0);
+        }();
+        const uint64_t range = range_env ? range_env : sc;
         CodeState::DevGrouped g{};
         e = upload_groups(cs, pl, dev, &g);
         if (e) return e;
-        for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
-            uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
-            const uint32_t maxd = pl.gstage_maxd[s];
-            while (b < end) {
-                uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
-                dim3 grid(n * tiles);
-                switch (vw) {
-                case 16: launch_gexec<16>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
-                case 8: launch_gexec<8>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
-                case 4: launch_gexec<4>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
-                case 2: launch_gexec<2>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
-                default: launch_gexec<1>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc); break;
+        for (uint64_t r0 = 0; r0 < sc; r0 += range) {
+            const uint64_t r1 = std::min<uint64_t>(sc, r0 + range);
+            const uint32_t tiles = uint32_t(((r1 - r0) / 16 + 1 + kExecBlock - 1) / kExecBlock);
+            for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
+                uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
+                const uint32_t maxd = pl.gstage_maxd[s];
+                while (b < end) {
+                    uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
+                    dim3 grid(n * tiles);
+                    launch_gexec<16>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc, r0, r1);
+                    CLAY_HIP(hipGetLastError());
+                    launches++;
+                    b += n;
                 }
-                CLAY_HIP(hipGetLastError());
-                launches++;
-                b += n;
             }
         }
         t_last_launches += launches;
