@@ -90,6 +90,16 @@ def _ptr(x) -> int:
     return int(x)
 
 
+_EXEC_MODES = {"ops": 0, "grouped": 1, "fused": 2}
+
+
+def set_exec_mode(mode: str) -> str:
+    """Plan executor for decode / repair / staged encode: 'grouped' (default) | 'fused' | 'ops'.
+    Returns the previous mode."""
+    prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])
+    return {v: k for k, v in _EXEC_MODES.items()}[prev]
+
+
 def set_encode_path(mode: str, tile: int = 0) -> str:
     """'auto' | 'staged' | 'fused' | 'bitsliced' | 'bitsliced2' -- process-wide encode path selection
     (`tile` overrides the bit-sliced tile width in 32-byte lanes; 0 = default)."""

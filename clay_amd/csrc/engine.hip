@@ -147,6 +147,124 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused tile executor: the whole grouped plan per tile of W byte positions, U
+// plane and re-read intermediates in LDS (no workspace round trips through HBM).
+// A lane group of W/16 lanes runs one group (16 bytes per lane); all lane groups
+// of the workgroup sweep a level's groups, then a barrier separates levels --
+// the same read-before-write order as one launch per level.  LDS = GF perm
+// tables (256 x 8 dwords) + nslots x W bytes (slots reused across levels).
+// ---------------------------------------------------------------------------
+constexpr int kFxBlock = 512;
+constexpr int kFxBatch = 8;
+struct FxArgs {
+    const DevGroup *groups;
+    const DevSrc *srcs, *dsts;
+    const int32_t *src_lds, *dst_lds;  // LDS slot (-1: global source / no slot)
+    const uint32_t *dst_glb;          // 1: also store to the global region
+    const uint32_t *coef;
+    const uint2 *pcoef;               // per source: its coefficient for dst d in byte d (8 dsts max)
+    const uint32_t *tabs;
+    const uint32_t *stage_begin;
+    uint32_t nstages, W, ntiles, pad;
+    uint64_t sc;
+};
+
+template <int MAXD>
+__global__ __launch_bounds__(kFxBlock) void k_fexec(ExecPtrs P, FxArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *ltab = reinterpret_cast<uint32_t *>(lds);
+    uint8_t *slots = lds + 256 * 8 * 4;
+    for (uint32_t i = threadIdx.x; i < 256 * 8; i += kFxBlock) ltab[i] = a.tabs[i];
+    const uint32_t LG = a.W / 16, nlg = kFxBlock / LG, lg = threadIdx.x / LG, li = threadIdx.x - lg * LG;
+    __syncthreads();
+    for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        const uint64_t pos = uint64_t(tile) * a.W + uint64_t(li) * 16;
+        const uint32_t nb = pos >= a.sc ? 0u : uint32_t(a.sc - pos < 16 ? a.sc - pos : 16);
+        for (uint32_t st = 0; st < a.nstages; st++) {
+            const uint32_t gend = a.stage_begin[st + 1];
+            for (uint32_t gi = a.stage_begin[st] + lg; gi < gend; gi += nlg) {
+                const DevGroup g = a.groups[gi];
+                uint32_t acc[MAXD][4];
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) acc[d][0] = acc[d][1] = acc[d][2] = acc[d][3] = 0;
+                // sources in batches of kFxBatch: every load of a batch is issued before
+                // the first multiply, so HBM latency is paid once per batch
+                for (uint32_t s0 = 0; s0 < g.nsrc; s0 += kFxBatch) {
+                    uint32_t v[kFxBatch][4];
+                    uint2 cb[kFxBatch];
+#pragma unroll
+                    for (int b = 0; b < kFxBatch; b++) {
+                        const uint32_t s = s0 + b;
+                        v[b][0] = v[b][1] = v[b][2] = v[b][3] = 0;
+                        cb[b] = make_uint2(0, 0);
+                        if (s < g.nsrc) {
+                            cb[b] = a.pcoef[g.src_begin + s];
+                            const int32_t sl = a.src_lds[g.src_begin + s];
+                            if (sl >= 0) {
+                                const uint4 x = *reinterpret_cast<const uint4 *>(slots + uint32_t(sl) * a.W + li * 16);
+                                v[b][0] = x.x; v[b][1] = x.y; v[b][2] = x.z; v[b][3] = x.w;
+                            } else {
+                                const DevSrc src = a.srcs[g.src_begin + s];
+                                const uint8_t *sp = P.p[src.base] + uint64_t(src.slot) * a.sc + pos;
+                                if (nb == 16) {
+                                    __builtin_memcpy(v[b], sp, 16);
+                                } else {
+                                    uint8_t tb[16] = {};
+                                    for (uint32_t i = 0; i < nb; i++) tb[i] = sp[i];
+                                    __builtin_memcpy(v[b], tb, 16);
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int b = 0; b < kFxBatch; b++) {
+                        const uint32_t s = s0 + b;
+                        if (s >= g.nsrc) break;
+                        GfIdx ix[4];
+#pragma unroll
+                        for (int w = 0; w < 4; w++) ix[w] = gf_idx(v[b][w]);
+#pragma unroll
+                        for (int d = 0; d < MAXD; d++) {
+                            if (d >= int(g.ndst)) break;
+                            const uint32_t c = ((d < 4 ? cb[b].x : cb[b].y) >> (8 * (d & 3))) & 0xffu;
+                            if (c == 1) {
+#pragma unroll
+                                for (int w = 0; w < 4; w++) acc[d][w] ^= v[b][w];
+                            } else {
+                                const GfTab t = load_tab(ltab + c * 8);
+#pragma unroll
+                                for (int w = 0; w < 4; w++) acc[d][w] ^= gf_mul_idx(ix[w], t);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) {
+                    if (d >= int(g.ndst)) break;
+                    const int32_t dl = a.dst_lds[g.dst_begin + d];
+                    if (dl >= 0)
+                        *reinterpret_cast<uint4 *>(slots + uint32_t(dl) * a.W + li * 16) =
+                            make_uint4(acc[d][0], acc[d][1], acc[d][2], acc[d][3]);
+                    if (a.dst_glb[g.dst_begin + d] && nb) {
+                        const DevSrc dst = a.dsts[g.dst_begin + d];
+                        uint8_t *dp = P.p[dst.base] + uint64_t(dst.slot) * a.sc + pos;
+                        if (nb == 16) {
+                            __builtin_memcpy(dp, acc[d], 16);
+                        } else {
+                            uint8_t tb[16];
+                            __builtin_memcpy(tb, acc[d], 16);
+                            for (uint32_t i = 0; i < nb; i++) dp[i] = tb[i];
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Fused encode (parity = last y-section).  See file header and DESIGN.md.
 // LDS: acc[p][z][W] bytes (p < Q parity rows, z < alpha layers, W positions).
@@ -331,6 +449,14 @@ struct DevState {
 };
 static DevState g_dev[64];
 
+// Fused-tile program for a plan (built once per plan, per device).
+struct FxProg {
+    bool ok = false;
+    uint32_t W = 0, nslots = 0, maxd = 1;
+    size_t lds = 0;
+    FxArgs dev{};
+};
+
 struct CodeState {
     clay_code_t code{};
     RsCtx rs;
@@ -343,6 +469,7 @@ struct CodeState {
         const uint32_t *coef;
     };
     std::map<std::pair<const Plan *, int>, DevGrouped> gplan;
+    std::map<std::pair<const Plan *, int>, FxProg> fplan;
     std::map<int, uint32_t *> mtab;
     explicit CodeState(const clay_code_t &c) : code(c), rs(c) {}
 };
@@ -442,16 +569,6 @@ static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::De
     return Error{};
 }
 
-// CLAY_EXEC=ops selects the one-op-per-block executor (k_exec) for A/B runs.
-static bool exec_grouped() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("CLAY_EXEC");
-        v = (e && std::strcmp(e, "ops") == 0) ? 0 : 1;
-    }
-    return v == 1;
-}
-
 template <int VW>
 static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
@@ -465,6 +582,158 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
         k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
     else
         k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
+}
+
+
+static constexpr size_t kFxLdsCap = 150 * 1024;
+
+static void build_fx(const Plan &pl, FxProg &fx, std::vector<int32_t> &src_lds, std::vector<int32_t> &dst_lds,
+                     std::vector<uint32_t> &dst_glb) {
+    const size_t ns = pl.gstage_begin.size() - 1;
+    const uint32_t ubase = 2 * pl.tn;
+    auto rk = [](const DevSrc &d) { return (uint64_t(d.base) << 32) | d.slot; };
+    std::map<uint64_t, int> first_w, last_use;
+    for (size_t st = 0; st < ns; st++)
+        for (uint32_t gi = pl.gstage_begin[st]; gi < pl.gstage_begin[st + 1]; gi++) {
+            const DevGroup &g = pl.groups[gi];
+            for (uint32_t d = 0; d < g.ndst; d++) {
+                uint64_t r = rk(pl.gdsts[g.dst_begin + d]);
+                if (!first_w.count(r)) first_w[r] = int(st);
+                last_use[r] = std::max(last_use.count(r) ? last_use[r] : 0, int(st));
+            }
+        }
+    std::map<uint64_t, bool> read_after;
+    for (size_t st = 0; st < ns; st++)
+        for (uint32_t gi = pl.gstage_begin[st]; gi < pl.gstage_begin[st + 1]; gi++) {
+            const DevGroup &g = pl.groups[gi];
+            for (uint32_t s = 0; s < g.nsrc; s++) {
+                uint64_t r = rk(pl.gsrcs[g.src_begin + s]);
+                auto it = first_w.find(r);
+                if (it == first_w.end()) continue;
+                if (it->second >= int(st)) return;  // read before its first write: not expressible
+                read_after[r] = true;
+                last_use[r] = std::max(last_use[r], int(st));
+            }
+        }
+    // interval colouring of the regions that are read back: [first write, last use]
+    std::vector<std::pair<int, uint64_t>> order;
+    for (auto &kv : first_w)
+        if (read_after.count(kv.first)) order.push_back({kv.second, kv.first});
+    std::sort(order.begin(), order.end());
+    std::vector<int> slot_end;  // per slot: last level it is busy
+    std::map<uint64_t, int32_t> slot_of;
+    for (auto &o : order) {
+        int sl = -1;
+        for (size_t i = 0; i < slot_end.size(); i++)
+            if (slot_end[i] < o.first) { sl = int(i); break; }
+        if (sl < 0) { sl = int(slot_end.size()); slot_end.push_back(0); }
+        slot_end[sl] = last_use[o.second];
+        slot_of[o.second] = sl;
+    }
+    fx.nslots = uint32_t(slot_end.size());
+    // widest tile that still lets 2 workgroups share a CU, else the widest that fits
+    for (size_t cap : {size_t(64 * 1024), kFxLdsCap}) {
+        for (uint32_t W : {2048u, 1024u, 512u, 256u, 128u, 64u}) {
+            size_t need = 256 * 8 * 4 + size_t(fx.nslots) * W;
+            if (need <= cap) { fx.W = W; fx.lds = need; break; }
+        }
+        if (fx.W) break;
+    }
+    if (!fx.W) return;
+    src_lds.resize(pl.gsrcs.size());
+    for (size_t i = 0; i < pl.gsrcs.size(); i++) {
+        auto it = slot_of.find(rk(pl.gsrcs[i]));
+        src_lds[i] = it == slot_of.end() ? -1 : it->second;
+        if (it == slot_of.end() && first_w.count(rk(pl.gsrcs[i]))) return;
+    }
+    dst_lds.resize(pl.gdsts.size());
+    dst_glb.resize(pl.gdsts.size());
+    for (size_t i = 0; i < pl.gdsts.size(); i++) {
+        auto it = slot_of.find(rk(pl.gdsts[i]));
+        dst_lds[i] = it == slot_of.end() ? -1 : it->second;
+        dst_glb[i] = pl.gdsts[i].base != ubase;  // U never leaves the chip; C / OUT regions always written
+    }
+    for (uint32_t m : pl.gstage_maxd) fx.maxd = std::max(fx.maxd, m);
+    fx.ok = true;
+}
+
+// Executor for plans: 0 = k_exec (one op per block), 1 = k_gexec grouped (default),
+// 2 = k_fexec fused tile executor when the plan fits LDS.  Initial value from
+// CLAY_EXEC ("ops" | "grouped" | "fused"); clay_set_exec_mode() overrides.
+static int g_exec_mode = [] {
+    const char *e = getenv("CLAY_EXEC");
+    return !e ? 1 : std::strcmp(e, "ops") == 0 ? 0 : std::strcmp(e, "fused") == 0 ? 2 : 1;
+}();
+static int exec_mode() { return g_exec_mode; }
+
+static Error run_fused(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
+                       const ExecPtrs &ptrs, size_t sc, bool *done) {
+    *done = false;
+    auto key = std::make_pair(&pl, dev);
+    auto it = cs.fplan.find(key);
+    if (it == cs.fplan.end()) {
+        FxProg fx;
+        std::vector<int32_t> sl, dl;
+        std::vector<uint32_t> dg;
+        build_fx(pl, fx, sl, dl, dg);
+        if (fx.ok) {
+            std::vector<uint2> pc(pl.gsrcs.size(), uint2{0, 0});
+            for (const DevGroup &gr : pl.groups)
+                for (uint32_t si = 0; si < gr.nsrc; si++)
+                    for (uint32_t d = 0; d < gr.ndst && d < 8; d++) {
+                        uint32_t c = pl.gcoef[gr.coef_begin + d * gr.nsrc + si] & 0xffu;
+                        if (d < 4) pc[gr.src_begin + si].x |= c << (8 * d);
+                        else pc[gr.src_begin + si].y |= c << (8 * (d - 4));
+                    }
+            const uint2 *dpc;
+            Error e0 = upload_vec(pc, &dpc);
+            if (e0) return e0;
+            fx.dev.pcoef = dpc;
+            CodeState::DevGrouped g{};
+            Error e = upload_groups(cs, pl, dev, &g);
+            if (e) return e;
+            const int32_t *dsl, *ddl;
+            const uint32_t *ddg, *dstb;
+            if ((e = upload_vec(sl, &dsl)) || (e = upload_vec(dl, &ddl)) || (e = upload_vec(dg, &ddg)) ||
+                (e = upload_vec(pl.gstage_begin, &dstb)))
+                return e;
+            fx.dev.groups = g.groups;
+            fx.dev.srcs = g.srcs;
+            fx.dev.dsts = g.dsts;
+            fx.dev.coef = g.coef;
+            fx.dev.src_lds = dsl;
+            fx.dev.dst_lds = ddl;
+            fx.dev.dst_glb = ddg;
+            fx.dev.stage_begin = dstb;
+            fx.dev.nstages = uint32_t(pl.gstage_begin.size() - 1);
+        }
+        if (getenv("CLAY_FX_DEBUG"))
+            fprintf(stderr, "[clay fx] ok=%d W=%u slots=%u lds=%zu maxd=%u stages=%zu groups=%zu\n", int(fx.ok), fx.W,
+                    fx.nslots, fx.lds, fx.maxd, pl.gstage_begin.size() - 1, pl.groups.size());
+        it = cs.fplan.emplace(key, fx).first;
+    }
+    FxProg &fx = it->second;
+    if (!fx.ok) return Error{};
+    FxArgs a = fx.dev;
+    a.tabs = ds.d_tabs;
+    a.W = fx.W;
+    a.sc = sc;
+    a.ntiles = uint32_t((sc + fx.W - 1) / fx.W);
+    const int per_cu = fx.lds <= 64 * 1024 ? 2 : 1;
+    const uint32_t grid = std::min<uint32_t>(a.ntiles, uint32_t(256 * per_cu * (1024 / kFxBlock)));
+    auto launch = [&](auto kern) -> Error {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     int(kFxLdsCap)));
+        kern<<<dim3(grid), dim3(kFxBlock), fx.lds, stream>>>(ptrs, a);
+        CLAY_HIP(hipGetLastError());
+        return Error{};
+    };
+    Error e = fx.maxd <= 1 ? launch(k_fexec<1>) : fx.maxd <= 2 ? launch(k_fexec<2>)
+            : fx.maxd <= 4 ? launch(k_fexec<4>) : launch(k_fexec<8>);
+    if (e) return e;
+    t_last_launches += 1;
+    *done = true;
+    return Error{};
 }
 
 static Error ensure_ws(DevState &ds, void *stream, size_t bytes, void **out) {
@@ -496,6 +765,11 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     const DevSrc *d_srcs;
     Error e = upload_plan(cs, pl, dev, &d_ops, &d_srcs);
     if (e) return e;
+    if (exec_mode() == 2 && pl.gstage_begin.size() == pl.stage_begin.size()) {
+        bool done = false;
+        e = run_fused(cs, pl, dev, ds, stream, ptrs, sc, &done);
+        if (e || done) return e;
+    }
     if (pl.uses_u) {
         void *ws = nullptr;
         e = ensure_ws(ds, stream, size_t(pl.tn) * chunk_for_ws, &ws);
@@ -509,7 +783,7 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     const uint64_t per_thread = uint64_t(vw);
     const uint32_t tiles = uint32_t((sc / per_thread + kExecBlock - 1) / kExecBlock);
     size_t launches = 0;
-    if (exec_grouped() && pl.gstage_begin.size() == pl.stage_begin.size()) {
+    if (exec_mode() >= 1 && pl.gstage_begin.size() == pl.stage_begin.size()) {
         // 16 bytes per lane regardless of sc / pointer alignment (see k_gexec).
         // CLAY_EXEC_RANGE=B runs all stages over byte range [r0, r0+B) of every
         // sub-chunk before the next range (cache-resident U round trips).
@@ -1405,6 +1679,13 @@ int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, con
 // size w), one device encode of that piece, and one 2D copy of each parity piece
 // back.  Pieces round-robin over `ns` streams, so H2D of piece p+1, the encode of
 // piece p and the D2H of piece p-1 overlap (PCIe is full duplex).
+int clay_set_exec_mode(int mode) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int prev = g_exec_mode;
+    if (mode >= 0 && mode <= 2) g_exec_mode = mode;
+    return prev;
+}
+
 int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *data_chunks,
                                uint8_t *const *parity_chunks, size_t chunk, int device, size_t piece_bytes,
                                int n_streams, clay_error_t *err) {

@@ -187,6 +187,12 @@ int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int devic
  * previous low-byte mode. */
 int clay_set_encode_path(int mode);
 
+/* Plan executor for decode / repair / staged encode (process-wide; tests and
+ * benchmarks): 0 = one op per block (k_exec), 1 = source-sharing op groups
+ * (k_gexec, default), 2 = fused tile executor with the U plane in LDS (k_fexec;
+ * plans that do not fit LDS run grouped).  Returns the previous mode. */
+int clay_set_exec_mode(int mode);
+
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
 const char *clay_last_encode_path(void);
 

@@ -32,6 +32,14 @@ def _auto_path():
     set_encode_path("auto")
 
 
+@pytest.fixture(params=["grouped", "fused", "ops"])
+def exec_mode(request):
+    """Run a test under each plan executor (k_gexec default, k_fexec, k_exec)."""
+    prev = clay_amd.set_exec_mode(request.param)
+    yield request.param
+    clay_amd.set_exec_mode(prev)
+
+
 @pytest.mark.parametrize("cfg", CONFIGS)
 @pytest.mark.parametrize("size_kind", ["empty", "tiny", "ragged", "aligned16", "sc2", "big"])
 def test_encode_matches_oracle(oracle_mod, cfg, size_kind):
@@ -110,7 +118,7 @@ def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_encode_fused_equals_staged(oracle_mod, cfg):
+def test_encode_fused_equals_staged(oracle_mod, cfg, exec_mode):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     data = rand_bytes(7, k * c.sub_chunk_no * 2 * 16 - 5)  # sc = 32: fused-eligible
@@ -128,7 +136,7 @@ def test_encode_fused_equals_staged(oracle_mod, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_decode_random_inputs_match_oracle(oracle_mod, cfg):
+def test_decode_random_inputs_match_oracle(oracle_mod, cfg, exec_mode):
     """Non-codeword inputs: only the reference's exact RS row choice reproduces these bytes."""
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
@@ -154,7 +162,7 @@ def test_decode_roundtrip_max_erasures(oracle_mod, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_repair_every_node_matches_oracle(oracle_mod, cfg):
+def test_repair_every_node_matches_oracle(oracle_mod, cfg, exec_mode):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     data = rand_bytes(5, k * c.sub_chunk_no * 2 * 3)
@@ -328,7 +336,7 @@ def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda):
 
 @pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13)])
 @pytest.mark.parametrize("sc", [16 * 257 + 2, 16 * 1000 + 9, 16 * 3001])
-def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc):
+def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc, exec_mode):
     """Sub-chunks spanning several executor tiles whose regions start at 2-byte / odd
     offsets (the (9,3,11) 256 MiB chunk has sc = 3,314,018): random (non-codeword)
     inputs, decode and repair byte-identical to the oracle."""
