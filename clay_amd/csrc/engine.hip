@@ -39,6 +39,7 @@ namespace clay {
 constexpr int kMaxTn = 64;                 // internal nodes supported on device
 constexpr int kMaxBases = 2 * kMaxTn + 2;  // C[tn], H[tn], U, OUT
 constexpr int kExecBlock = 256;
+constexpr int kGxBatch = 4;
 constexpr int kFusedBlock = 512;
 constexpr size_t kFusedLdsBudget = 128 * 1024;
 
@@ -87,9 +88,26 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                                                       const DevSrc *__restrict__ gdsts,
                                                       const uint32_t *__restrict__ gcoef,
                                                       const uint32_t *__restrict__ tabs, uint32_t g0,
-                                                      uint32_t tiles, uint64_t sc, uint64_t r0, uint64_t r1) {
+                                                      uint32_t tiles, uint64_t sc, uint64_t r0, uint64_t r1,
+                                                      uint32_t ngroups, uint32_t order, uint32_t bx) {
     constexpr int NW = (VW + 3) / 4;
-    const uint32_t gi = blockIdx.x / tiles, tile = blockIdx.x - gi * tiles;
+    // Block -> (group, tile).  order 0: group-major.  1: tile-major -- all groups of a
+    // tile run back to back, so an input sub-chunk tile read by several groups is
+    // re-read while still in L2 / MALL.  2: tile-major within contiguous per-XCD
+    // block ranges (blocks round-robin over the 8 XCDs: xcd = blockIdx % 8).
+    uint32_t gi, tile;
+    if (order == 0) {
+        gi = blockIdx.x / tiles;
+        tile = blockIdx.x - gi * tiles;
+    } else {
+        uint32_t v = blockIdx.x;
+        if (order == 2) {
+            v = (blockIdx.x & 7u) * bx + (blockIdx.x >> 3);
+            if (v >= ngroups * tiles) return;
+        }
+        tile = v / ngroups;
+        gi = v - tile * ngroups;
+    }
     const DevGroup g = groups[g0 + gi];
     const uint64_t pos = r0 + (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
     if (pos >= r1) return;
@@ -104,31 +122,45 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     for (int d = 0; d < MAXD; d++)
 #pragma unroll
         for (int w = 0; w < NW; w++) acc[d][w] = 0;
-    for (uint32_t s = 0; s < g.nsrc; ++s) {
-        const DevSrc src = gsrcs[g.src_begin + s];
-        const uint8_t *sp = P.p[src.base] + uint64_t(src.slot) * sc + pos;
-        Words<NW> v;
-        if (full) {
-            __builtin_memcpy(&v, sp, sizeof(v));
-        } else {
-            uint8_t tb[NW * 4] = {};
-            for (uint32_t i = 0; i < nb; i++) tb[i] = sp[i];
-            __builtin_memcpy(&v, tb, sizeof(v));
+    // kGxBatch source loads in flight before the first multiply (memory-level parallelism)
+    for (uint32_t s0 = 0; s0 < g.nsrc; s0 += kGxBatch) {
+        Words<NW> v[kGxBatch];
+#pragma unroll
+        for (int b = 0; b < kGxBatch; b++) {
+            const uint32_t s = s0 + b;
+#pragma unroll
+            for (int w = 0; w < NW; w++) v[b].w[w] = 0;
+            if (s < g.nsrc) {
+                const DevSrc src = gsrcs[g.src_begin + s];
+                const uint8_t *sp = P.p[src.base] + uint64_t(src.slot) * sc + pos;
+                if (full) {
+                    __builtin_memcpy(&v[b], sp, sizeof(v[b]));
+                } else {
+                    uint8_t tb[NW * 4] = {};
+                    for (uint32_t i = 0; i < nb; i++) tb[i] = sp[i];
+                    __builtin_memcpy(&v[b], tb, sizeof(v[b]));
+                }
+            }
         }
-        GfIdx ix[NW];
 #pragma unroll
-        for (int w = 0; w < NW; w++) ix[w] = gf_idx(v.w[w]);
+        for (int b = 0; b < kGxBatch; b++) {
+            const uint32_t s = s0 + b;
+            if (s >= g.nsrc) break;
+            GfIdx ix[NW];
 #pragma unroll
-        for (int d = 0; d < MAXD; d++) {
-            if (d >= int(g.ndst)) break;
-            const uint32_t c = gcoef[g.coef_begin + d * g.nsrc + s];
-            if (c == 1) {
+            for (int w = 0; w < NW; w++) ix[w] = gf_idx(v[b].w[w]);
 #pragma unroll
-                for (int w = 0; w < NW; w++) acc[d][w] ^= v.w[w];
-            } else {
-                const GfTab t = load_tab(tabs + c * 8);
+            for (int d = 0; d < MAXD; d++) {
+                if (d >= int(g.ndst)) break;
+                const uint32_t c = gcoef[g.coef_begin + d * g.nsrc + s];
+                if (c == 1) {
 #pragma unroll
-                for (int w = 0; w < NW; w++) acc[d][w] ^= gf_mul_idx(ix[w], t);
+                    for (int w = 0; w < NW; w++) acc[d][w] ^= v[b].w[w];
+                } else {
+                    const GfTab t = load_tab(tabs + c * 8);
+#pragma unroll
+                    for (int w = 0; w < NW; w++) acc[d][w] ^= gf_mul_idx(ix[w], t);
+                }
             }
         }
     }
@@ -572,16 +604,22 @@ static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::De
 template <int VW>
 static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
-                         uint64_t sc, uint64_t r0, uint64_t r1) {
+                         uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n) {
     dim3 block(kExecBlock);
+    static const uint32_t order = [] {
+        const char *e = getenv("CLAY_GEXEC_ORDER");
+        return e ? uint32_t(atoi(e)) : 2u;
+    }();
+    const uint32_t nb = n * tiles, bx = (nb + 7) / 8;
+    if (order == 2) grid = dim3(8 * bx);
     if (maxd <= 1)
-        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
+        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
     else if (maxd <= 2)
-        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
+        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
     else if (maxd <= 4)
-        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
+        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
     else
-        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1);
+        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
 }
 
 
@@ -804,7 +842,7 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
                 while (b < end) {
                     uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
                     dim3 grid(n * tiles);
-                    launch_gexec<16>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc, r0, r1);
+                    launch_gexec<16>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc, r0, r1, n);
                     CLAY_HIP(hipGetLastError());
                     launches++;
                     b += n;
