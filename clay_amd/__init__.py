@@ -271,6 +271,20 @@ class ClayCode:
         if rc:
             _raise(rc, err)
 
+    def repair_device_full_chunks(self, lost_node: int, helper_ids: Sequence[int], helper_chunks,
+                                  chunk_size: int, out, device: int = 0, stream: int = 0):
+        """Repair from whole helper chunks resident on the device (clay.h
+        clay_repair_device_full_chunks): no gather of the beta repair layers."""
+        ids = list(helper_ids)
+        hp = (C.c_void_p * max(1, len(ids)))(*[_ptr(x) for x in helper_chunks])
+        err = ClayErrorStruct()
+        rc = _lib.lib().clay_repair_device_full_chunks(C.byref(self._c), int(lost_node), _sizes(ids),
+                                                       hp, len(ids), int(chunk_size),
+                                                       C.c_void_p(_ptr(out)), int(device),
+                                                       C.c_void_p(int(stream)), C.byref(err))
+        if rc:
+            _raise(rc, err)
+
     def repair_device(self, lost_node: int, helper_ids: Sequence[int], helper_bufs, chunk_size: int,
                       out, device: int = 0, stream: int = 0):
         ids = list(helper_ids)

@@ -1496,7 +1496,8 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
 }
 
 static Error repair_device_impl(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs,
-                                const size_t *lens, size_t nh, size_t chunk, uint8_t *out, int dev, void *stream) {
+                                const size_t *lens, size_t nh, size_t chunk, uint8_t *out, int dev, void *stream,
+                                bool full = false) {
     Error e = check_code(code);
     if (e) return e;
     const clay_code_t &c = *code;
@@ -1519,10 +1520,11 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
     std::vector<uint8_t> key(hin);
     key.push_back(uint8_t(lost & 0xFF));
     key.push_back(uint8_t(lost >> 8));
+    key.push_back(uint8_t(full));
     auto it = cs.rep.find(key);
     if (it == cs.rep.end()) {
         std::unique_ptr<Plan> p;
-        e = plan_repair(c, cs.rs, lost, hin, slot_of, sub, p);
+        e = plan_repair(c, cs.rs, lost, hin, slot_of, sub, p, full);
         if (e) return e;
         it = cs.rep.emplace(key, std::move(p)).first;
     }
@@ -1641,6 +1643,14 @@ int clay_repair_device(const clay_code_t *code, size_t lost, const size_t *ids, 
                        size_t chunk, uint8_t *out, int device, void *stream, clay_error_t *err) {
     if (err) std::memset(err, 0, sizeof(*err));
     Error e = repair_device_impl(code, lost, ids, bufs, nullptr, nh, chunk, out, device, stream);
+    return e ? report(e, err) : 0;
+}
+
+int clay_repair_device_full_chunks(const clay_code_t *code, size_t lost, const size_t *ids,
+                                   const uint8_t *const *chunks, size_t nh, size_t chunk, uint8_t *out, int device,
+                                   void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = repair_device_impl(code, lost, ids, chunks, nullptr, nh, chunk, out, device, stream, true);
     return e ? report(e, err) : 0;
 }
 

@@ -476,7 +476,8 @@ Error plan_decode(const clay_code_t &c, RsCtx &rs, const std::vector<uint8_t> &e
 
 // repair.rs:140-421
 Error plan_repair(const clay_code_t &c, RsCtx &rs, size_t lost, const std::vector<uint8_t> &hin,
-                  const std::vector<long> &slot_of_id, const std::vector<size_t> &ridx, std::unique_ptr<Plan> &out) {
+                  const std::vector<long> &slot_of_id, const std::vector<size_t> &ridx, std::unique_ptr<Plan> &out,
+                  bool full_chunks) {
     (void)slot_of_id;
     if (rs.init_err)
         return make_error(CLAY_ERR_RECONSTRUCTION_FAILED, 0, 0, 0, "RS reconstruction failed: RS init failed: %s",
@@ -493,7 +494,11 @@ Error plan_repair(const clay_code_t &c, RsCtx &rs, size_t lost, const std::vecto
         if (i != li && !hin[i] && !is_shortened(c, i)) aloof[i] = 1;
     std::vector<long> pind(alpha, -1);
     for (size_t i = 0; i < ridx.size(); i++) pind[ridx[i]] = long(i);
-    auto H = [&](size_t node, size_t z) { return rkey(RK_H, uint32_t(node), uint32_t(pind[z])); };
+    // helper payload slot: position in the beta-sub-chunk list (repair.rs:225-240), or
+    // layer z itself when the helpers are whole chunks (device-side gather)
+    auto H = [&](size_t node, size_t z) {
+        return rkey(RK_H, uint32_t(node), uint32_t(full_chunks ? long(z) : pind[z]));
+    };
     auto U = [](size_t node, size_t z) { return rkey(RK_U, uint32_t(node), uint32_t(z)); };
     auto OUT = [](size_t z) { return rkey(RK_OUT, 0, uint32_t(z)); };
     std::vector<size_t> zv(t), ord(ridx.size());

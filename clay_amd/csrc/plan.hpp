@@ -121,6 +121,6 @@ Error plan_decode(const clay_code_t &c, RsCtx &rs, const std::vector<uint8_t> &e
 // repair.rs:140-421 with the given helper set (internal ids) and index list.
 Error plan_repair(const clay_code_t &c, RsCtx &rs, size_t lost, const std::vector<uint8_t> &helper_int,
                   const std::vector<long> &slot_of_id, const std::vector<size_t> &subchunks,
-                  std::unique_ptr<Plan> &out);
+                  std::unique_ptr<Plan> &out, bool full_chunks = false);
 
 }  // namespace clay

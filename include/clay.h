@@ -166,6 +166,16 @@ int clay_repair_device(const clay_code_t *code, size_t lost_node, const size_t *
                        const uint8_t *const *helper_bufs, size_t n_helpers, size_t chunk_size,
                        uint8_t *out, int device, void *stream, clay_error_t *err);
 
+/* Repair on device from WHOLE helper chunks (device pointers, chunk_size bytes
+ * each): the kernels read the beta repair layers of repair.rs:22-49 in place, so
+ * callers holding full chunks in HBM skip the gather/concat that
+ * minimum_to_repair's index lists imply (repair.rs:61-126).
+ * Same output bytes as clay_repair on the gathered sub-chunks. */
+int clay_repair_device_full_chunks(const clay_code_t *code, size_t lost_node, const size_t *helper_ids,
+                                   const uint8_t *const *helper_chunks, size_t n_helpers,
+                                   size_t chunk_size, uint8_t *out, int device, void *stream,
+                                   clay_error_t *err);
+
 /* ------------------------------------------------------------------ */
 /* Engine control / introspection                                      */
 /* ------------------------------------------------------------------ */

@@ -83,6 +83,13 @@ def repair_cfg(k, m, d, chunk, lost):
     ms, mn = timed(lambda: c.repair_device(lost, helpers, [hb[i] for i in range(len(helpers))], chunk, out, 0,
                                            stream.cuda_stream))
     report(f"repair ({k},{m},{d}) chunk {chunk} node {lost}", ms, mn, len(helpers) * beta * sc + chunk)
+    del hb
+    # same repair straight from whole helper chunks in HBM (only the beta layers are read)
+    full = rnd(len(helpers), chunk, 4)
+    ms, mn = timed(lambda: c.repair_device_full_chunks(lost, helpers, [full[i] for i in range(len(helpers))],
+                                                       chunk, out, 0, stream.cuda_stream))
+    report(f"repair ({k},{m},{d}) chunk {chunk} node {lost} from full chunks", ms, mn,
+           len(helpers) * beta * sc + chunk)
 
 
 if __name__ == "__main__":

@@ -377,3 +377,26 @@ def test_encode_host_pipelined_matches_oracle(oracle_mod, torch_cuda, cfg, sc, p
     pn = [np.zeros(chunk, np.uint8) for _ in range(m)]
     c.encode_host_pipelined(dn, pn, chunk, 0, piece, streams)
     assert all(np.array_equal(pn[j], ref[k + j]) for j in range(m))
+
+
+@pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13), (6, 3, 8)])
+def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg, exec_mode):
+    """Repair straight from whole helper chunks in HBM (no gather): same bytes as the
+    oracle's repair on the gathered beta sub-chunks, for codewords and random chunks."""
+    torch = torch_cuda
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    sc = 16 * 40 + 6
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc + k)
+    code_chunks = c.encode_array(rand_bytes(k, k * chunk))
+    for chunks in (code_chunks, rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)):
+        dev = torch.from_numpy(np.ascontiguousarray(chunks)).cuda()
+        for lost in sorted({0, k - 1, c.n - 1}):
+            avail = [i for i in range(c.n) if i != lost]
+            info = c.minimum_to_repair(lost, avail)
+            out = torch.zeros(chunk, dtype=torch.uint8, device="cuda")
+            c.repair_device_full_chunks(lost, [h for h, _ in info], [dev[h] for h, _ in info], chunk, out)
+            torch.cuda.synchronize()
+            pd = {h: np.concatenate([chunks[h][z * sc:(z + 1) * sc] for z in idx]) for h, idx in info}
+            assert out.cpu().numpy().tobytes() == o.repair(lost, pd, chunk), (cfg, lost)
