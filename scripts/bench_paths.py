@@ -59,6 +59,17 @@ def encode_cfg(k, m, d, stripe):
     report(f"encode ({k},{m},{d}) {stripe >> 20} MiB", ms, mn, (k + m) * chunk)
 
 
+def encode_batch_cfg(k, m, d, stripe, n):
+    """clay_bench.rs shape (1 MiB stripes) as one device batch call: n stripes per call."""
+    c = ClayCode(k, m, d)
+    chunk = c.encoded_chunk_size(stripe)
+    data, par = rnd(n * k, chunk, 5), torch.empty((n * m, chunk), dtype=torch.uint8, device="cuda")
+    dl, pl = [data[i] for i in range(n * k)], [par[i] for i in range(n * m)]
+    ms, mn = timed(lambda: c.encode_device_batch(dl, pl, n, chunk, 0, stream.cuda_stream))
+    report(f"encode ({k},{m},{d}) batch {n} x {stripe >> 10} KiB", ms, mn, n * (k + m) * chunk,
+           {"input_GiBps": round(n * k * chunk / (ms * 1e-3) / 2**30, 1)})
+
+
 def decode_cfg(k, m, d, stripe, er):
     c = ClayCode(k, m, d)
     chunk = c.encoded_chunk_size(stripe)
@@ -95,6 +106,7 @@ def repair_cfg(k, m, d, chunk, lost):
 if __name__ == "__main__":
     encode_cfg(10, 4, 13, 1 << 30)
     encode_cfg(4, 2, 5, 64 << 20)
+    encode_batch_cfg(4, 2, 5, 1 << 20, 256)
     decode_cfg(4, 2, 5, 64 << 20, [0])
     decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])
     decode_cfg(10, 4, 13, 1 << 30, [0])
