@@ -63,6 +63,37 @@ def latest_traffic():
         return None, None
 
 
+def cpu_baseline_threads(seconds: float, threads: int):
+    """Stripe-parallel oracle encode on `threads` host cores (the reference
+    itself is single-threaded; this is the all-cores CPU figure beside it)."""
+    import threading
+    from oracle import oracle  # checker/baseline only
+    c = oracle.OracleClay(K, M, D)
+    sample = 64 << 20
+    data = np.random.default_rng(1).integers(0, 256, sample, dtype=np.uint8)
+    c.encode_array(data)  # warm (lazy GF tables) before threads start
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(i):
+        while time.perf_counter() < stop:
+            c.encode_array(data)
+            counts[i] += 1
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    padded = c.encoded_chunk_size(sample) * K
+    n = sum(counts)
+    return {"value": round(n * padded / el / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x (10,4,13) encode of 64 MiB stripes on {threads} threads in {el:.1f}s, "
+                      f"oracle/clay_oracle.c via ctypes (GIL released)"}
+
+
 def cpu_baseline(seconds: float):
     from oracle import oracle  # checker/baseline only
     oracle.build()
@@ -212,6 +243,8 @@ def main():
     }
     if world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline_all_cores"] = cpu_baseline_threads(args.cpu_seconds / 2,
+                                                             min(16, os.cpu_count() or 1))
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -89,7 +89,8 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                                                       const uint32_t *__restrict__ gcoef,
                                                       const uint32_t *__restrict__ tabs, uint32_t g0,
                                                       uint32_t tiles, uint64_t sc, uint64_t r0, uint64_t r1,
-                                                      uint32_t ngroups, uint32_t order, uint32_t bx) {
+                                                      uint32_t ngroups, uint32_t order, uint32_t bx,
+                                                      uint8_t *const *__restrict__ ptab) {
     constexpr int NW = (VW + 3) / 4;
     // Block -> (group, tile).  order 0: group-major.  1: tile-major -- all groups of a
     // tile run back to back, so an input sub-chunk tile read by several groups is
@@ -132,7 +133,8 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
             for (int w = 0; w < NW; w++) v[b].w[w] = 0;
             if (s < g.nsrc) {
                 const DevSrc src = gsrcs[g.src_begin + s];
-                const uint8_t *sp = P.p[src.base] + uint64_t(src.slot) * sc + pos;
+                const uint8_t *sp = (ptab ? ptab[blockIdx.y * kMaxBases + src.base] : P.p[src.base]) +
+                                    uint64_t(src.slot) * sc + pos;
                 if (full) {
                     __builtin_memcpy(&v[b], sp, sizeof(v[b]));
                 } else {
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     for (int d = 0; d < MAXD; d++) {
         if (d >= int(g.ndst)) break;
         const DevSrc dst = gdsts[g.dst_begin + d];
-        uint8_t *dp = P.p[dst.base] + uint64_t(dst.slot) * sc + pos;
+        uint8_t *dp = (ptab ? ptab[blockIdx.y * kMaxBases + dst.base] : P.p[dst.base]) + uint64_t(dst.slot) * sc + pos;
         if (full) {
             __builtin_memcpy(dp, acc[d], sizeof(acc[d]));
         } else {
@@ -478,6 +480,7 @@ struct DevState {
     std::mutex pipe_mu;
     std::vector<hipStream_t> pipe_streams;
     std::vector<Workspace> pipe_bufs;
+    std::map<void *, Workspace> batch_tab;  // device pointer tables of batched launches, per stream
 };
 static DevState g_dev[64];
 
@@ -604,7 +607,8 @@ static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::De
 template <int VW>
 static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
-                         uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n) {
+                         uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n, uint8_t *const *ptab = nullptr,
+                         uint32_t nstripes = 1) {
     dim3 block(kExecBlock);
     static const uint32_t order = [] {
         const char *e = getenv("CLAY_GEXEC_ORDER");
@@ -612,14 +616,15 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
     }();
     const uint32_t nb = n * tiles, bx = (nb + 7) / 8;
     if (order == 2) grid = dim3(8 * bx);
+    grid.y = nstripes;
     if (maxd <= 1)
-        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
+        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
     else if (maxd <= 2)
-        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
+        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
     else if (maxd <= 4)
-        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
+        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
     else
-        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx);
+        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
 }
 
 
@@ -1400,6 +1405,65 @@ static Error encode_staged(CodeState &cs, DevState &ds, int dev, const uint8_t *
     return Error{};
 }
 
+// Batched small stripes: every level of the staged encode plan
+// runs for ALL stripes in one k_gexec launch (grid.y = stripe), pointers from a
+// device table of kMaxBases entries per stripe; U workspace per stripe.
+static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uint8_t *const *data,
+                                 uint8_t *const *par, size_t n_stripes, size_t chunk, hipStream_t stream) {
+    const clay_code_t &c = cs.code;
+    const uint32_t tn = uint32_t(c.q * c.t);
+    if (!cs.enc) {
+        Error e = plan_encode(c, cs.rs, cs.enc);
+        if (e) return e;
+    }
+    const Plan &pl = *cs.enc;
+    CodeState::DevGrouped g{};
+    Error e = upload_groups(cs, pl, dev, &g);
+    if (e) return e;
+    void *ws = nullptr;
+    if (pl.uses_u) {
+        e = ensure_ws(ds, stream, n_stripes * tn * chunk, &ws);
+        if (e) return e;
+    }
+    std::vector<uint8_t *> tab(n_stripes * kMaxBases, nullptr);
+    for (size_t s = 0; s < n_stripes; s++) {
+        uint8_t **t = &tab[s * kMaxBases];
+        for (size_t i = 0; i < c.k; i++) t[i] = const_cast<uint8_t *>(data[s * c.k + i]);
+        for (size_t i = 0; i < c.m; i++) t[c.k + c.nu + i] = par[s * c.m + i];
+        if (ws) t[2 * tn] = static_cast<uint8_t *>(ws) + s * tn * chunk;
+    }
+    // the table buffer is reused across calls: drain earlier batches on this stream first
+    Workspace &tb = ds.batch_tab[stream];
+    const size_t bytes = tab.size() * sizeof(uint8_t *);
+    CLAY_HIP(hipStreamSynchronize(stream));
+    if (tb.bytes < bytes) {
+        if (tb.ptr) CLAY_HIP(hipFree(tb.ptr));
+        tb.ptr = nullptr;
+        tb.bytes = 0;
+        CLAY_HIP(hipMalloc(&tb.ptr, bytes));
+        tb.bytes = bytes;
+    }
+    CLAY_HIP(hipMemcpy(tb.ptr, tab.data(), bytes, hipMemcpyHostToDevice));
+    const uint64_t sc = chunk / c.sub_chunk_no;
+    const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+    ExecPtrs P{};
+    size_t launches = 0;
+    for (size_t st = 0; st + 1 < pl.gstage_begin.size(); st++) {
+        uint32_t b = pl.gstage_begin[st], end = pl.gstage_begin[st + 1];
+        while (b < end) {
+            uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
+            launch_gexec<16>(pl.gstage_maxd[st], dim3(n * tiles), stream, P, g, ds.d_tabs, b, tiles, sc, 0, sc, n,
+                             static_cast<uint8_t *const *>(tb.ptr), uint32_t(n_stripes));
+            CLAY_HIP(hipGetLastError());
+            launches++;
+            b += n;
+        }
+    }
+    t_last_launches += launches;
+    t_last_path = "staged-batch";
+    return Error{};
+}
+
 static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *data, uint8_t *const *par,
                                 size_t n_stripes, size_t chunk, int dev, void *stream) {
     Error e = check_code(code);
@@ -1423,6 +1487,11 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
         return make_error(CLAY_ERR_RECONSTRUCTION_FAILED, 0, 0, 0, "RS reconstruction failed: RS init failed: %s",
                           rs_error_name(cs.rs.init_err));
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // many small stripes: one launch per plan level for the whole batch instead of
+    // one launch per stripe (launch-bound below ~4 MiB of data per stripe)
+    if (g_encode_mode == 0 && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) && n_stripes <= 65535 &&
+        code->q * code->t <= size_t(kMaxTn))
+        return encode_staged_batch(cs, *ds, dev, data, par, n_stripes, chunk, st);
     if (g_encode_mode == 0 || g_encode_mode >= 3) {
         bool done = false;
         e = encode_bitsliced(cs, dev, data, par, n_stripes, chunk, st, &done);

@@ -400,3 +400,24 @@ def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg, e
             torch.cuda.synchronize()
             pd = {h: np.concatenate([chunks[h][z * sc:(z + 1) * sc] for z in idx]) for h, idx in info}
             assert out.cpu().numpy().tobytes() == o.repair(lost, pd, chunk), (cfg, lost)
+
+
+@pytest.mark.parametrize("cfg", [(4, 2, 5), (10, 4, 13), (9, 3, 11), (6, 3, 8), (5, 3, 6)])
+@pytest.mark.parametrize("sc,n", [(32, 4), (16 * 70 + 6, 9), (4096, 5)])
+def test_encode_device_batch_small_stripes(oracle_mod, torch_cuda, cfg, sc, n):
+    """Batched small stripes: one launch per plan level for the whole batch (grid.y =
+    stripe, device pointer table); every stripe's parity equals the oracle's."""
+    torch = torch_cuda
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    chunk = c.sub_chunk_no * sc
+    refs = [o.encode_array(rand_bytes(100 * s + sc, k * chunk)) for s in range(n)]
+    data = torch.from_numpy(np.concatenate([r[:k] for r in refs])).cuda()
+    par = torch.zeros((n * m, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device_batch([data[i] for i in range(n * k)], [par[i] for i in range(n * m)], n, chunk)
+    torch.cuda.synchronize()
+    if k * chunk <= 4 << 20:  # small stripes batch; larger ones keep the per-stripe kernels
+        assert last_encode_path() == "staged-batch"
+    got = par.cpu().numpy()
+    for s in range(n):
+        assert np.array_equal(got[s * m:(s + 1) * m], refs[s][k:]), (cfg, sc, n, s)
