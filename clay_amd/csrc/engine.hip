@@ -1821,11 +1821,11 @@ int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *da
     for (size_t i = 0; i < c.m; i++)
         if (!parity_chunks[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk"), err);
     const size_t alpha = c.sub_chunk_no, sc = chunk / alpha, K = c.k, M = c.m;
-    size_t w = piece_bytes ? piece_bytes : (size_t(32) << 20) / (K * alpha);
+    size_t w = piece_bytes ? piece_bytes : (size_t(128) << 20) / (K * alpha);  // sweep: r01 host pipeline
     w = w >= 256 ? w / 256 * 256 : (w + 7) / 8 * 8;  // whole 256-byte encode tiles (8-byte minimum)
     w = std::max<size_t>(8, std::min(w, sc));
     const size_t np = (sc + w - 1) / w;
-    const int ns = int(std::max<size_t>(1, std::min<size_t>(np, n_streams > 0 ? size_t(n_streams) : 3)));
+    const int ns = int(std::max<size_t>(1, std::min<size_t>(np, n_streams > 0 ? size_t(n_streams) : 2)));
     DevState *ds;
     {
         std::lock_guard<std::mutex> lk(g_mu);

@@ -139,9 +139,9 @@ int clay_encode_device_batch(const clay_code_t *code, const uint8_t *const *data
 /* Host-streaming encode (host memory in, host memory out; blocking).  data_chunks:
  * k host pointers, parity_chunks: m host pointers (chunk_size bytes each; pin
  * them, e.g. hipHostMalloc / hipHostRegister, for overlap).  The stripe is cut
- * into pieces of piece_bytes (0 = auto, ~32 MiB of input per piece) of every
+ * into pieces of piece_bytes (0 = auto, ~128 MiB of input per piece) of every
  * sub-chunk; each piece is copied in with one 2D copy per node, encoded on the
- * device and its parity copied out, round-robin over n_streams (0 = 3) streams
+ * device and its parity copied out, round-robin over n_streams (0 = 2) streams
  * so H2D, encode and D2H of consecutive pieces overlap.  Same parity bytes as
  * clay_encode / clay_encode_device.  Replaces the host-side entry of
  * ClayCode::encode (lib.rs:165-167 -> encode.rs:30-80) for callers that hold
