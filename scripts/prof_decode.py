@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""One decode (10,4,13) 1 GiB with 4 erasures {0,4,8,12} (and optionally repair (9,3,11)),
+repeated --iters times, for rocprofv3 --pmc passes (HBM bytes of the grouped executor)."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from clay_amd import ClayCode  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=4)
+ap.add_argument("--what", default="decode4")
+args = ap.parse_args()
+if args.what == "decode4":
+    c = ClayCode(10, 4, 13)
+    chunk = c.encoded_chunk_size(1 << 30)
+    er = [0, 4, 8, 12]
+    full = torch.randint(0, 256, (c.n, chunk), dtype=torch.uint8, device="cuda")
+    outs = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
+    ins = [None if i in er else full[i] for i in range(c.n)]
+    ous = [outs[i] if i in er else None for i in range(c.n)]
+    fn = lambda: c.decode_device(ins, er, ous, chunk)  # noqa: E731
+else:
+    c = ClayCode(9, 3, 11)
+    chunk = 268_435_458
+    sc = chunk // c.sub_chunk_no
+    info = c.minimum_to_repair(0, list(range(1, 12)))
+    hs = [h for h, _ in info]
+    hb = torch.randint(0, 256, (len(hs), len(info[0][1]) * sc), dtype=torch.uint8, device="cuda")
+    out = torch.empty(chunk, dtype=torch.uint8, device="cuda")
+    fn = lambda: c.repair_device(0, hs, [hb[i] for i in range(len(hs))], chunk, out)  # noqa: E731
+for _ in range(args.iters):
+    fn()
+torch.cuda.synchronize()
+print("done", args.what, args.iters)
