@@ -122,7 +122,13 @@ void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
                          merged.end());
             ops[i].src = std::move(merged);
         }
-        if (is_out[i] || ops[i].src.size() > 2) continue;
+        if (is_out[i]) continue;
+        const size_t ns = ops[i].src.size(), r = rl[i].size();
+        static const int cost_env = [] {
+            const char *e = getenv("CLAY_PLAN_FOLD_COST");
+            return e ? atoi(e) : -1;
+        }();
+        const int cost_fold = cost_env >= 0 ? cost_env : fold_cost;
         // sources: never-written inputs (any reader count), or final versions of
         // computed regions when at most 2 ops read this one (folding then never
         // adds HBM reads: 2 + 1 + r round-trip bytes vs 2r direct).
@@ -132,7 +138,10 @@ void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
             auto it = cur.find(t.key);
             finals &= t.ver < 0 ? !written.count(t.key) : (it != cur.end() && it->second == t.ver);
         }
-        if (inputs || (finals && rl[i].size() <= 2)) inl[i] = 1;
+        if (ns <= 2 && (inputs || (finals && r <= 2))) inl[i] = 1;
+        // traffic model: r consumer layers each re-read ns sources, against ns reads +
+        // 1 write + r reads of the materialised region
+        else if (cost_fold && finals && r * ns <= ns + 1 + r && ns <= size_t(cost_fold)) inl[i] = 1;
     }
 }
 

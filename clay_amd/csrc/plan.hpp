@@ -92,6 +92,11 @@ class PlanBuilder {
     std::vector<Op> ops;
     std::unordered_map<uint64_t, int32_t> cur;  // region -> current version
     std::vector<uint8_t> zero_c, zero_h;          // per internal node: C / H input is known zero
+    // >0: also fold ops over final versions with up to fold_cost sources when the
+    // consumer-layer count says it saves HBM traffic (CLAY_PLAN_FOLD_COST).  Off:
+    // at 32 it cut decode traffic 3.49 -> 3.27 GB but measured slower (0.91 -> 1.01 ms,
+    // wider groups), and repair's per-layer consumer groups break the estimate.
+    int fold_cost = 0;
 
     // dst = XOR coef*src; terms on zero regions / zero coefs are dropped.
     void emit(uint64_t dst, const std::vector<std::pair<uint64_t, uint8_t>> &terms);
