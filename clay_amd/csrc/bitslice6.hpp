@@ -187,6 +187,12 @@ __device__ __forceinline__ void st16s(const uint8_t *sbase, uint32_t voff, uint3
     // overwrite the data VGPRs before the store has read them)
     asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
 }
+// same with the non-temporal hint: parity is written once and never re-read by the kernel
+__device__ __forceinline__ void st16s_nt(const uint8_t *sbase, uint32_t voff, uint32_t a, uint32_t b, uint32_t c,
+                                         uint32_t d) {
+    const u32x4 v = {a, b, c, d};
+    asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
+}
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field)
 __device__ __forceinline__ void wait_vm_rt(int n) {
@@ -200,7 +206,7 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     }
 }
 
-template <int KD, int M, int PARTS, bool EARLY>
+template <int KD, int M, int PARTS, bool EARLY, bool NTS = false>
 struct Bs6Kernel {
     using S = Shape<KD, M>;
     using MP = v6::Map<PARTS>;
@@ -430,8 +436,13 @@ struct Bs6Kernel {
         asm volatile("" : "+v"(off));
         off += pos;
         if (!ragged) {
-            st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
-            st16s(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
+            if constexpr (NTS) {
+                st16s_nt(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
+                st16s_nt(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
+            } else {
+                st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
+                st16s(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
+            }
         } else {
             uint8_t *p = a.par[X] + off;
 #pragma unroll
@@ -498,9 +509,9 @@ struct Bs6Kernel {
     }
 };
 
-template <int KD, int M, int PARTS, bool EARLY>
-__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY>::BLOCK)) void k_bs6_encode(BsArgs a) {
-    using Kn = Bs6Kernel<KD, M, PARTS, EARLY>;
+template <int KD, int M, int PARTS, bool EARLY, bool NTS = false>
+__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void k_bs6_encode(BsArgs a) {
+    using Kn = Bs6Kernel<KD, M, PARTS, EARLY, NTS>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int c = int(threadIdx.x) >> Kn::PB, part = int(threadIdx.x) & (PARTS - 1);

@@ -1132,10 +1132,10 @@ static Error launch_bs5(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     return Error{};
 }
 
-template <int KD, int M, int PARTS, bool EARLY>
+template <int KD, int M, int PARTS, bool EARLY, bool NTS = false>
 static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
                         size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs6Kernel<KD, M, PARTS, EARLY>;
+    using Kn = bs::Bs6Kernel<KD, M, PARTS, EARLY, NTS>;
     using S = typename Kn::S;
     const clay_code_t &c = cs.code;
     if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
@@ -1149,7 +1149,7 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     int dev = 0;
     CLAY_HIP(hipGetDevice(&dev));
     if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS, EARLY>),
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS, EARLY, NTS>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
         attr[dev] = true;
     }
@@ -1163,12 +1163,12 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
         a.tiles_per_xcd = (a.ntiles + 7) / 8;
         const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
         a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs6_encode<KD, M, PARTS, EARLY><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        bs::k_bs6_encode<KD, M, PARTS, EARLY, NTS><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
         CLAY_HIP(hipGetLastError());
         t_last_launches++;
     }
     char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced6-k%dm%d-w%d%s", KD, M, Kn::W, EARLY ? "e" : "");
+    std::snprintf(buf, sizeof(buf), "bitsliced6-k%dm%d-w%d%s%s", KD, M, Kn::W, EARLY ? "e" : "", NTS ? "-nts" : "");
     t_last_path = buf;
     *done = true;
     return Error{};
@@ -1342,11 +1342,13 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     // (auto's first choice for (10,4,13)); tile override 4 = 128-byte tiles / 5-slot ring
     if (g_encode_mode == 8 || (g_encode_mode == 0 && g_bs_pg == 0)) {
         if (key == 1004) {
-            // tile override: 4 / 8 parts (128 / 256-byte tiles), +16 = early slot release
+            // tile override: 4 / 8 parts (128 / 256-byte tiles), +16 = early slot release,
+            // 40 = 256-byte tiles with non-temporal parity stores
             switch (g_bs_pg) {
             case 4: e = launch_bs6<10, 4, 4, false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             case 20: e = launch_bs6<10, 4, 4, true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             case 24: e = launch_bs6<10, 4, 8, true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+            case 40: e = launch_bs6<10, 4, 8, false, true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             default: e = launch_bs6<10, 4, 8, false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
             }
         }

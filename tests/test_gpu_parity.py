@@ -96,7 +96,7 @@ def test_bitsliced23_encode_matches_oracle(oracle_mod, cfg, scale, variant):
     assert np.array_equal(got, ref), (cfg, scale)
 
 
-@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6", "bitsliced6:4", "bitsliced6:20", "bitsliced6:24",
+@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6", "bitsliced6:4", "bitsliced6:20", "bitsliced6:24", "bitsliced6:40",
                                      "bitsliced7", "bitsliced7:1", "bitsliced8"])
 @pytest.mark.parametrize("sc", [64, 72, 104, 128, 1064, 6440, 64 * 300 + 40, 64 * 2000 + 8])
 def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
