@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kExecBlock) void k_exec(ExecPtrs P, const DevOp *__
 // Grouped staged executor: one workgroup = one source-sharing op group x one tile.
 // Each source tile is loaded once, split into its perm-table indices once, and
 // multiplied into up to MAXD destination accumulators (dst_d = XOR_s coef[d][s] * src_s).
-template <int VW, int MAXD>
+template <int VW, int MAXD, bool BATCH = false>
 __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup *__restrict__ groups,
                                                       const DevSrc *__restrict__ gsrcs,
                                                       const DevSrc *__restrict__ gdsts,
@@ -133,8 +133,12 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
             for (int w = 0; w < NW; w++) v[b].w[w] = 0;
             if (s < g.nsrc) {
                 const DevSrc src = gsrcs[g.src_begin + s];
-                const uint8_t *sp = (ptab ? ptab[blockIdx.y * kMaxBases + src.base] : P.p[src.base]) +
-                                    uint64_t(src.slot) * sc + pos;
+                // BATCH (template, so the single-stripe kernel keeps its kernarg pointer table)
+                const uint8_t *sp;
+                if constexpr (BATCH)
+                    sp = ptab[blockIdx.y * kMaxBases + src.base] + uint64_t(src.slot) * sc + pos;
+                else
+                    sp = P.p[src.base] + uint64_t(src.slot) * sc + pos;
                 if (full) {
                     __builtin_memcpy(&v[b], sp, sizeof(v[b]));
                 } else {
@@ -170,7 +174,11 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     for (int d = 0; d < MAXD; d++) {
         if (d >= int(g.ndst)) break;
         const DevSrc dst = gdsts[g.dst_begin + d];
-        uint8_t *dp = (ptab ? ptab[blockIdx.y * kMaxBases + dst.base] : P.p[dst.base]) + uint64_t(dst.slot) * sc + pos;
+        uint8_t *dp;
+        if constexpr (BATCH)
+            dp = ptab[blockIdx.y * kMaxBases + dst.base] + uint64_t(dst.slot) * sc + pos;
+        else
+            dp = P.p[dst.base] + uint64_t(dst.slot) * sc + pos;
         if (full) {
             __builtin_memcpy(dp, acc[d], sizeof(acc[d]));
         } else {
@@ -618,13 +626,13 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
     if (order == 2) grid = dim3(8 * bx);
     grid.y = nstripes;
     if (maxd <= 1)
-        k_gexec<VW, 1><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
+        (ptab ? k_gexec<VW, 1, true> : k_gexec<VW, 1, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
     else if (maxd <= 2)
-        k_gexec<VW, 2><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
+        (ptab ? k_gexec<VW, 2, true> : k_gexec<VW, 2, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
     else if (maxd <= 4)
-        k_gexec<VW, 4><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
+        (ptab ? k_gexec<VW, 4, true> : k_gexec<VW, 4, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
     else
-        k_gexec<VW, 8><<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
+        (ptab ? k_gexec<VW, 8, true> : k_gexec<VW, 8, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
 }
 
 

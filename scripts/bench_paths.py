@@ -103,7 +103,21 @@ def repair_cfg(k, m, d, chunk, lost):
            len(helpers) * beta * sc + chunk)
 
 
+def prewarm(ms=250.0):
+    """Untimed load so every configuration is timed at the GPU's sustained clock."""
+    import time
+    c = ClayCode(10, 4, 13)
+    chunk = c.encoded_chunk_size(1 << 30)
+    data, par = rnd(10, chunk, 9), torch.empty((4, chunk), dtype=torch.uint8, device="cuda")
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):
+            c.encode_device([data[i] for i in range(10)], [par[i] for i in range(4)], chunk, 0, stream.cuda_stream)
+        torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
+    prewarm(float(os.environ.get("PREWARM_MS", "250")))
     encode_cfg(10, 4, 13, 1 << 30)
     encode_cfg(4, 2, 5, 64 << 20)
     encode_batch_cfg(4, 2, 5, 1 << 20, 256)
