@@ -39,7 +39,7 @@ namespace clay {
 constexpr int kMaxTn = 64;                 // internal nodes supported on device
 constexpr int kMaxBases = 2 * kMaxTn + 2;  // C[tn], H[tn], U, OUT
 constexpr int kExecBlock = 256;
-constexpr int kGxBatch = 4;
+constexpr int kGxBatch = 4;  // 8 measured slower (decode 4 erasures 0.87 -> 0.97 ms)
 constexpr int kFusedBlock = 512;
 constexpr size_t kFusedLdsBudget = 128 * 1024;
 
