@@ -4,17 +4,22 @@
 One step = encode of one 1 GiB stripe (the reference's ClayCode::encode of
 1,073,741,824 bytes pads to 1,073,745,920 = 10 chunks of 107,374,592 bytes)
 whose data chunks are already resident in HBM; parity (4 chunks) is written to
-HBM.  Multi-GPU: one process per GPU (torchrun), each rank encodes its own
-stripe (stripes are independent -> no data-path collective; weak scaling).  The
+HBM.  Multi-GPU: one process per GPU, each rank encodes its own stripe (stripes
+are independent, encode.rs:30-80 -> no data-path collective; weak scaling).  The
 barrier / max-time reduction are timing plumbing only.
 
-value       = stripes * padded stripe bytes / max-over-ranks wall time, GiB/s
+    python bench.py                      # N = 1
+    python bench.py --gpus 8             # spawns 8 ranks itself (no torchrun needed)
+    torchrun --nproc-per-node 8 bench.py --gpus 8   # same, launched externally
+
+value       = ranks * padded stripe bytes * steps / max-over-ranks wall time, GiB/s
 roofline    = algorithmic bytes per launch (read 10 + write 4 chunks =
               1,503,244,288 B) / mean kernel time (HIP events on the launch
               stream) vs 8 TB/s HBM peak
 cpu_baseline= the oracle (C restatement of the reference CPU path: scalar
               PRT/PFT + AVX2 RS region multiply, single thread) on a bounded
-              sample of the same workload.
+              sample of the same workload, rank 0 at N = 1 only; cfg1 adds the
+              reference's own bench shape, (4,2,5) on 1 MiB (clay_bench.rs:20-56).
 """
 from __future__ import annotations
 
@@ -22,6 +27,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,9 +40,10 @@ sys.path.insert(0, ROOT)
 K, M, D = 10, 4, 13
 STRIPE_BYTES = 1 << 30  # reference ClayCode::encode input
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+VERIFY_W = 4096         # positions per verified column slice (every rank, both ends)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -46,16 +54,204 @@ def parse():
                          "load to ramp: 5 warmups gave 0.44 ms/launch, 200 gave 0.385)")
     ap.add_argument("--stripe-bytes", type=int, default=STRIPE_BYTES)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="bound on the CPU-baseline sample (0 disables)")
+                    help="bound on the headline CPU-baseline sample (0 disables all CPU legs)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-small", action="store_true", help="skip the clay_bench-size GPU batch rates")
     ap.add_argument("--path", default="auto",
-                    choices=["auto", "fused", "staged", "bitsliced", "bitsliced2", "bitsliced3", "bitsliced4", "bitsliced5", "bitsliced6"])
-    return ap.parse_args()
+                    choices=["auto", "fused", "staged", "bitsliced", "bitsliced6", "stream"])
+    ap.add_argument("--tile", type=int, default=0, help="encode path variant (clay_set_encode_path)")
+    ap.add_argument("--cpu-dry", action="store_true",
+                    help="test mode without a GPU: the oracle replaces the device encode, gloo "
+                         "replaces RCCL; everything else (launcher, ranks, timing, JSON) is the same")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher: `--gpus N` without an external torchrun spawns N fresh rank processes
+# before this process touches HIP (never exec from a GPU-initialised process)
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv) -> int:
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(args.gpus),
+                    "LOCAL_WORLD_SIZE": str(args.gpus), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        r = p.wait()
+        rc = rc or r
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# CPU baselines (oracle = the reference CPU path restated in C; checker / baseline only)
+# ---------------------------------------------------------------------------
+def host_info() -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=5).stdout.strip())
+    except Exception:
+        nproc = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "nproc": nproc,
+            "affinity_cpus": affinity, "omp_num_threads": int(omp) if omp and omp.isdigit() else None}
+
+
+def all_cores_threads(info: dict) -> int:
+    """Threads for the all-cores CPU figure: the CPUs this process may run on, bounded by the
+    box's CPU share (OMP_NUM_THREADS is set to it on the GPU pool)."""
+    n = info["affinity_cpus"] or 1
+    if info["omp_num_threads"]:
+        n = min(n, info["omp_num_threads"])
+    return max(1, n)
+
+
+def _timed(fn, seconds: float, threads: int = 1):
+    """Run fn() repeatedly on `threads` threads for ~`seconds`; returns (calls, elapsed)."""
+    import threading
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(i):
+        while time.perf_counter() < stop:
+            fn()
+            counts[i] += 1
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return sum(counts), time.perf_counter() - t0
+
+
+def cpu_baseline_headline(seconds: float, threads: int):
+    """(10,4,13) encode on 64 MiB stripes of the same code: the reference is single-threaded
+    (no threads in the crate); the all-cores figure runs independent stripes in parallel
+    (ctypes releases the GIL)."""
+    from oracle import oracle  # checker / baseline only
+    oracle.build()
+    c = oracle.OracleClay(K, M, D)
+    sample = 64 << 20
+    data = np.random.default_rng(1).integers(0, 256, sample, dtype=np.uint8)
+    c.encode_array(data)  # warm (lazy GF tables)
+    padded = c.encoded_chunk_size(sample) * K
+    n1, e1 = _timed(lambda: c.encode_array(data), seconds, 1)
+    nt, et = _timed(lambda: c.encode_array(data), seconds / 2, threads)
+    one = {"value": round(n1 * padded / e1 / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+           "sample": f"{n1} x (10,4,13) encode of 64 MiB stripes in {e1:.1f}s, single thread, "
+                     f"oracle/clay_oracle.c (scalar PRT/PFT + AVX2 RS, as reed-solomon-erasure simd-accel)"}
+    allc = {"value": round(nt * padded / et / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{nt} x (10,4,13) encode of 64 MiB stripes on {threads} threads in {et:.1f}s"}
+    return one, allc
+
+
+def cpu_baseline_cfg1(seconds: float, threads: int):
+    """BASELINE.json configs[0]: ClayCode::encode of 1 MiB at (4,2,5) on the reference CPU path
+    (the criterion shape of benches/clay_bench.rs:20-56, data from a fixed seed), plus the same
+    file's decode (1 erasure, node 0, :58-93) and repair (node 0, :95-138) legs.  Throughput is
+    input bytes per second, as criterion's Throughput::Bytes(size)."""
+    from oracle import oracle
+    oracle.build()
+    k, m, d = 4, 2, 5
+    size = 1 << 20
+    c = oracle.OracleClay(k, m, d)
+    data = np.random.default_rng(42).integers(0, 256, size, dtype=np.uint8)
+    enc = c.encode_array(data)
+    chunk = enc.shape[1]
+    avail = {i: enc[i] for i in range(1, c.n)}
+    info = c.minimum_to_repair(0, list(range(1, c.n)))
+    sc = chunk // c.sub_chunk_no
+    helper = {h: np.concatenate([enc[h][z * sc:(z + 1) * sc] for z in idx]) for h, idx in info}
+    legs = {"encode": lambda: c.encode_array(data),
+            "decode_1_erasure": lambda: c.decode(avail, [0]),
+            "repair_node0": lambda: c.repair(0, helper, chunk)}
+    out = {"config": "(k=4,m=2,d=5) 1 MiB (clay_bench.rs shape), oracle/clay_oracle.c", "unit": "MiB/s",
+           "chunk_bytes": chunk, "sub_chunk_bytes": sc}
+    per = max(0.5, seconds / (2 * len(legs)))
+    for name, fn in legs.items():
+        fn()
+        n1, e1 = _timed(fn, per, 1)
+        nt, et = _timed(fn, per, threads)
+        out[name] = {"single_thread": round(n1 * size / e1 / 2**20, 2),
+                     "all_cores": round(nt * size / et / 2**20, 2), "cores": threads,
+                     "calls": [n1, nt], "seconds": [round(e1, 2), round(et, 2)]}
+    return out
+
+
+# ---------------------------------------------------------------------------
+# GPU legs
+# ---------------------------------------------------------------------------
+def verify_slices(code, data, par, chunk, oracle_cls):
+    """Parity of positions [0, w) and [sc - w, sc) of every sub-chunk against the oracle: each
+    byte offset is an independent codeword, so a column slice is a small stripe of its own."""
+    alpha = code.sub_chunk_no
+    sc = chunk // alpha
+    w = min(VERIFY_W, sc)
+    o = oracle_cls(K, M, D)
+    ok = True
+    for p0 in sorted({0, sc - w}):
+        d = data.view(K, alpha, sc)[:, :, p0:p0 + w].contiguous().cpu().numpy().reshape(-1)
+        ref = o.encode_array(d)
+        got = par.view(M, alpha, sc)[:, :, p0:p0 + w].contiguous().cpu().numpy().reshape(M, -1)
+        ok = ok and bool(np.array_equal(got, ref[K:]))
+    return ok
+
+
+def small_stripe_rates(torch, dev, local, sh):
+    """GPU batched encode at the reference bench sizes (clay_bench.rs:20-25, (4,2,5)): many
+    independent stripes per call through clay_encode_device_batch, device-resident."""
+    from clay_amd import ClayCode
+    import clay_amd
+    code = ClayCode(4, 2, 5)
+    out = {"config": "(k=4,m=2,d=5) clay_encode_device_batch, ~64 MiB of input per call", "unit": "GiB/s"}
+    for size in (1024, 10 * 1024, 100 * 1024, 1 << 20):
+        chunk = code.encoded_chunk_size(size)
+        n = max(4, (64 << 20) // (4 * chunk))
+        data = torch.randint(0, 256, (n * 4, chunk), dtype=torch.uint8, device=dev)
+        par = torch.empty((n * 2, chunk), dtype=torch.uint8, device=dev)
+        dp, pp = [data[i] for i in range(n * 4)], [par[i] for i in range(n * 2)]
+        for _ in range(3):
+            code.encode_device_batch(dp, pp, n, chunk, local, sh)
+        torch.cuda.synchronize(dev)
+        reps = 10
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            code.encode_device_batch(dp, pp, n, chunk, local, sh)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        out[f"{size}B"] = {"stripes_per_call": n, "GiBps": round(reps * n * size / el / 2**30, 2),
+                           "us_per_call": round(el / reps * 1e6, 1), "path": clay_amd.last_encode_path()}
+        del data, par
+    return out
 
 
 def latest_traffic():
-    """Per-launch HBM bytes from the newest committed PMC summary (profiles/*_pmc.json)."""
+    """Per-launch HBM bytes from the newest committed PMC summary (profiles/*encode*_pmc.json)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*encode*_pmc.json")))
     if not files:
         return None, None
@@ -67,157 +263,130 @@ def latest_traffic():
         return None, None
 
 
-def cpu_baseline_threads(seconds: float, threads: int):
-    """Stripe-parallel oracle encode on `threads` host cores (the reference
-    itself is single-threaded; this is the all-cores CPU figure beside it)."""
-    import threading
-    from oracle import oracle  # checker/baseline only
-    c = oracle.OracleClay(K, M, D)
-    sample = 64 << 20
-    data = np.random.default_rng(1).integers(0, 256, sample, dtype=np.uint8)
-    c.encode_array(data)  # warm (lazy GF tables) before threads start
-    counts = [0] * threads
-    stop = time.perf_counter() + seconds
-
-    def work(i):
-        while time.perf_counter() < stop:
-            c.encode_array(data)
-            counts[i] += 1
-
-    t0 = time.perf_counter()
-    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    el = time.perf_counter() - t0
-    padded = c.encoded_chunk_size(sample) * K
-    n = sum(counts)
-    return {"value": round(n * padded / el / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x (10,4,13) encode of 64 MiB stripes on {threads} threads in {el:.1f}s, "
-                      f"oracle/clay_oracle.c via ctypes (GIL released)"}
-
-
-def cpu_baseline(seconds: float):
-    from oracle import oracle  # checker/baseline only
-    oracle.build()
-    c = oracle.OracleClay(K, M, D)
-    sample = 64 << 20  # 64 MiB stripes of the same code, repeated
-    data = np.random.default_rng(1).integers(0, 256, sample, dtype=np.uint8)
-    c.encode_array(data)  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        c.encode_array(data)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    padded = c.encoded_chunk_size(sample) * K
-    return {"value": round(n * padded / el / 2**30, 4), "unit": "GiB/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{n} x (10,4,13) encode of 64 MiB stripes in {el:.1f}s, single thread, "
-                      f"oracle/clay_oracle.c (scalar PRT/PFT + AVX2 RS, as reed-solomon-erasure simd-accel)"}
-
-
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-
+def run_rank(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group("gloo" if args.cpu_dry else "nccl")
+    from oracle import oracle  # checker / CPU legs only (and the dry run's stand-in encode)
+    oracle.build()
 
-    import clay_amd
-    from clay_amd import ClayCode
-    clay_amd.set_encode_path(args.path)
-    code = ClayCode(K, M, D)
-    chunk = code.encoded_chunk_size(args.stripe_bytes)
+    ocode = oracle.OracleClay(K, M, D)
+    chunk = ocode.encoded_chunk_size(args.stripe_bytes)
     padded = chunk * K
-    sc = chunk // code.sub_chunk_no
+    alpha = ocode.sub_chunk_no
+    sc = chunk // alpha
+    path, launches = "oracle-cpu-dry", 0
+    verified = None
 
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    data = torch.randint(0, 256, (K, chunk), dtype=torch.uint8, device=dev, generator=g)
-    par = torch.empty((M, chunk), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
-    dptr = [data[i] for i in range(K)]
-    pptr = [par[i] for i in range(M)]
+    if args.cpu_dry:
+        host = np.random.default_rng(1234 + rank).integers(0, 256, padded, dtype=np.uint8)
+        step = lambda: ocode.encode_array(host)  # noqa: E731
+        sync = lambda: None  # noqa: E731
+        dev_t = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev_t = torch.device("cuda", local)
+        import clay_amd
+        from clay_amd import ClayCode
+        clay_amd.set_encode_path(args.path, args.tile)
+        code = ClayCode(K, M, D)
+        assert code.encoded_chunk_size(args.stripe_bytes) == chunk
+        g = torch.Generator(device=dev_t)
+        g.manual_seed(1234 + rank)
+        data = torch.randint(0, 256, (K, chunk), dtype=torch.uint8, device=dev_t, generator=g)
+        par = torch.empty((M, chunk), dtype=torch.uint8, device=dev_t)
+        stream = torch.cuda.current_stream(dev_t)
+        sh = stream.cuda_stream
+        dptr = [data[i] for i in range(K)]
+        pptr = [par[i] for i in range(M)]
+        step = lambda: code.encode_device(dptr, pptr, chunk, local, sh)  # noqa: E731
+        sync = lambda: torch.cuda.synchronize(dev_t)  # noqa: E731
+        t_pre = time.perf_counter()
+        while (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
+            for _ in range(8):
+                step()
+            sync()
 
-    t_pre = time.perf_counter()
-    while (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
-        for _ in range(8):
-            code.encode_device(dptr, pptr, chunk, local, sh)
-        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
-        code.encode_device(dptr, pptr, chunk, local, sh)
-    path = clay_amd.last_encode_path()
-    launches = clay_amd.last_launch_count()
-    torch.cuda.synchronize(dev)
+        step()
+    sync()
+    if not args.cpu_dry:
+        path = clay_amd.last_encode_path()
+        launches = clay_amd.last_launch_count()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # ---- timed region: exactly K steps between barrier + synchronize on both sides ----
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record(stream)
-        code.encode_device(dptr, pptr, chunk, local, sh)
-        evs[i][1].record(stream)
-    torch.cuda.synchronize(dev)
+        if not args.cpu_dry:
+            evs[i][0].record(stream)
+        step()
+        if not args.cpu_dry:
+            evs[i][1].record(stream)
+    sync()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if args.cpu_dry:
+        kern_ms = [el / args.steps * 1e3] * args.steps
+        verified = True
+    else:
+        kern_ms = [a.elapsed_time(b) for a, b in evs]
+        if not args.no_verify:
+            verified = verify_slices(code, data, par, chunk, oracle.OracleClay)
+
+    # per-rank wall / kernel mean / verified -> every rank (max over ranks is the job time)
+    mine = torch.tensor([el, float(np.mean(kern_ms)), 0.0 if verified is False else 1.0],
+                        dtype=torch.float64, device=dev_t)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per = [t.cpu().tolist() for t in allr]
+    else:
+        per = [mine.cpu().tolist()]
+    tmax = max(p[0] for p in per)
 
-    verified = None
-    if rank == 0 and world == 1 and not args.no_verify:
-        from oracle import oracle
-        oracle.build()
-        host = data.cpu().numpy().reshape(-1)
-        ref = oracle.OracleClay(K, M, D).encode_array(host[:padded])
-        verified = bool(np.array_equal(par.cpu().numpy(), ref[K:]))
-
-    host_incl = host_sync = None
-    if rank == 0 and world == 1 and not args.no_host_path:
-        # PCIe-inclusive (DESIGN.md): pinned host data chunks -> device -> parity back to pinned
-        # host memory.  host_sync: one stream, whole-stripe copies; host_incl: the pipelined
-        # host-streaming encode (clay_encode_host_pipelined, pieces over 3 streams).
-        hsrc = torch.empty((K, chunk), dtype=torch.uint8).pin_memory()
-        hdst = torch.empty((M, chunk), dtype=torch.uint8).pin_memory()
-        hsrc.copy_(data.cpu())
-        reps = 3
-        torch.cuda.synchronize(dev)
-        h0 = time.perf_counter()
-        for _ in range(reps):
-            data.copy_(hsrc, non_blocking=True)
-            code.encode_device(dptr, pptr, chunk, local, sh)
-            hdst.copy_(par, non_blocking=True)
-        torch.cuda.synchronize(dev)
-        host_sync = round(reps * padded / (time.perf_counter() - h0) / 2**30, 3)
-        hs, hd = [hsrc[i] for i in range(K)], [hdst[i] for i in range(M)]
-        code.encode_host_pipelined(hs, hd, chunk, local)  # warm (streams, piece buffers)
-        h0 = time.perf_counter()
-        for _ in range(reps):
-            code.encode_host_pipelined(hs, hd, chunk, local)
-        host_incl = round(reps * padded / (time.perf_counter() - h0) / 2**30, 3)
-        if verified is not None:
-            verified = verified and bool(torch.equal(hdst, par.cpu()))
+    host_incl = host_sync = small = None
+    if rank == 0 and world == 1 and not args.cpu_dry:
+        if not args.no_host_path:
+            # PCIe-inclusive: pinned host data chunks -> device -> parity back to
+            # pinned host memory.  host_sync: one stream, whole-stripe copies; host_incl: the
+            # pipelined host-streaming encode (clay_encode_host_pipelined, pieces over 3 streams).
+            hsrc = torch.empty((K, chunk), dtype=torch.uint8).pin_memory()
+            hdst = torch.empty((M, chunk), dtype=torch.uint8).pin_memory()
+            hsrc.copy_(data.cpu())
+            reps = 3
+            sync()
+            h0 = time.perf_counter()
+            for _ in range(reps):
+                data.copy_(hsrc, non_blocking=True)
+                step()
+                hdst.copy_(par, non_blocking=True)
+            sync()
+            host_sync = round(reps * padded / (time.perf_counter() - h0) / 2**30, 3)
+            hs, hd = [hsrc[i] for i in range(K)], [hdst[i] for i in range(M)]
+            code.encode_host_pipelined(hs, hd, chunk, local)  # warm (streams, piece buffers)
+            h0 = time.perf_counter()
+            for _ in range(reps):
+                code.encode_host_pipelined(hs, hd, chunk, local)
+            host_incl = round(reps * padded / (time.perf_counter() - h0) / 2**30, 3)
+            if verified is not None:
+                verified = verified and bool(torch.equal(hdst, par.cpu()))
+        if not args.no_small:
+            small = small_stripe_rates(torch, dev_t, local, sh)
 
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
-        return
+        return 0
 
     algo_bytes = padded + M * chunk  # read k chunks + write m chunks per launch
     mean_ms = float(np.mean(kern_ms))
@@ -235,29 +404,49 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (uniform random bytes, torch generator seed 1234+rank), device-resident",
+        "data": ("synthetic (uniform random bytes, seed 1234+rank), "
+                 + ("host memory, oracle stand-in encode (--cpu-dry)" if args.cpu_dry else "device-resident")),
         "config": {"workload": "(k=10,m=4,d=13) encode, one 1 GiB stripe per GPU",
                    "stripe_input_bytes": args.stripe_bytes, "padded_stripe_bytes": padded,
-                   "chunk_bytes": chunk, "sub_chunk_bytes": sc, "alpha": code.sub_chunk_no,
+                   "chunk_bytes": chunk, "sub_chunk_bytes": sc, "alpha": alpha,
                    "parallelism": f"stripe-per-gpu x{world}", "encode_path": path,
                    "launches_per_step": launches, "prewarm_ms": args.prewarm_ms},
+        "per_rank": {"wall_ms_per_step": [round(p[0] / args.steps * 1e3, 4) for p in per],
+                     "kernel_ms_mean": [round(p[1], 4) for p in per],
+                     "verified": [bool(p[2]) for p in per]},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_ms_mean": round(mean_ms, 4), "kernel_ms_min": round(min(kern_ms), 4)},
-        "verified_vs_oracle": verified,
+        "verified_vs_oracle": verified if world == 1 else all(bool(p[2]) for p in per),
         "host_inclusive_GiBps": host_incl,
         "host_inclusive_sync_GiBps": host_sync,
+        "gpu_small_stripes": small,
     }
+    if args.cpu_dry:
+        out["cpu_dry"] = True
     if world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        out["cpu_baseline_all_cores"] = cpu_baseline_threads(args.cpu_seconds / 2,
-                                                             min(16, os.cpu_count() or 1))
+        info = host_info()
+        threads = all_cores_threads(info)
+        one, allc = cpu_baseline_headline(args.cpu_seconds, threads)
+        out["cpu_baseline"] = one
+        out["cpu_baseline_all_cores"] = allc
+        out["cpu_baseline_cfg1"] = cpu_baseline_cfg1(min(args.cpu_seconds, 8.0), threads)
+        out["host"] = info
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args, argv)
+    return run_rank(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

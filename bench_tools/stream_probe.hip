@@ -1,0 +1,72 @@
+// stream_probe.hip -- where does the streaming encode kernel's time go?  Times
+// k_stream_encode on the BASELINE (10,4,13) 1 GiB stripe with parts switched off
+// (PROBE bits: 1 = no math, 2 = no DMA, 4 = no parity stores; the probes write wrong
+// bytes and exist only in this tool, never in libclay_amd.so).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o bench_tools/stream_probe bench_tools/stream_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "../clay_amd/csrc/stream_encode.hpp"
+
+using namespace clay::bs;
+
+template <int L, int PROBE>
+static float run(BsArgs a, int reps) {
+    using Kn = StreamEnc<10, L>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_stream_encode<10, L, PROBE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    std::vector<float> t;
+    for (int r = 0; r < reps; r++) {
+        (void)hipEventRecord(e0);
+        k_stream_encode<10, L, PROBE><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
+        (void)hipEventRecord(e1);
+        (void)hipEventSynchronize(e1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (r >= 3) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main() {
+    const uint32_t sc = 419432;
+    const size_t chunk = size_t(sc) * 256;
+    uint8_t *data, *par;
+    if (hipMalloc(&data, 10 * chunk) != hipSuccess || hipMalloc(&par, 4 * chunk) != hipSuccess) return 1;
+    (void)hipMemset(data, 7, 10 * chunk);
+    BsArgs a{};
+    for (int i = 0; i < 10; i++) a.data[i] = data + i * chunk;
+    for (int x = 0; x < 4; x++) a.par[x] = par + x * chunk;
+    a.sc = sc;
+    a.tiles_per_xcd = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
+    a.nslots = 32;
+    const double bytes = 14.0 * chunk;
+    auto rep = [&](const char *n, float ms) {
+        printf("%-34s %8.4f ms  %7.1f GB/s (algorithmic)\n", n, ms, bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    };
+    for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
+    (void)hipDeviceSynchronize();
+    for (int rr = 0; rr < 2; rr++) {
+        rep("L0 full", run<0, 0>(a, 15));
+        rep("L4 full", run<4, 0>(a, 15));
+        rep("L0 no math (memory only)", run<0, 1>(a, 15));
+        rep("L4 no math (memory only)", run<4, 1>(a, 15));
+        rep("L0 no math coalesced DMA", run<0, 9>(a, 15));
+        rep("L4 no math coalesced DMA", run<4, 9>(a, 15));
+        rep("L0 reads", run<0, 5>(a, 15));
+        rep("L4 reads", run<4, 5>(a, 15));
+        rep("L0 reads coalesced", run<0, 13>(a, 15));
+        rep("L4 reads coalesced", run<4, 13>(a, 15));
+        rep("L4 no DMA (math + stores)", run<4, 2>(a, 15));
+        rep("L4 stores only", run<4, 3>(a, 15));
+    }
+    return 0;
+}

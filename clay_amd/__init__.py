@@ -90,22 +90,22 @@ def _ptr(x) -> int:
     return int(x)
 
 
-_EXEC_MODES = {"ops": 0, "grouped": 1, "fused": 2}
-
-
-def set_exec_mode(mode: str) -> str:
-    """Plan executor for decode / repair / staged encode: 'grouped' (default) | 'fused' | 'ops'.
-    Returns the previous mode."""
-    prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])
-    return {v: k for k, v in _EXEC_MODES.items()}[prev]
+_ENCODE_PATHS = {"auto": 0, "staged": 1, "fused": 2, "bitsliced": 3, "bitsliced6": 4, "stream": 5}
 
 
 def set_encode_path(mode: str, tile: int = 0) -> str:
-    """'auto' | 'staged' | 'fused' | 'bitsliced' | 'bitsliced2' -- process-wide encode path selection
-    (`tile` overrides the bit-sliced tile width in 32-byte lanes; 0 = default)."""
-    modes = {"auto": 0, "staged": 1, "fused": 2, "bitsliced": 3, "bitsliced2": 4, "bitsliced3": 5, "bitsliced4": 6, "bitsliced5": 7, "bitsliced6": 8, "bitsliced7": 9, "bitsliced8": 10}
-    prev = _lib.lib().clay_set_encode_path(modes[mode] | (int(tile) << 8))
-    return {v: k for k, v in modes.items()}.get(prev, "auto")
+    """Process-wide encode path: 'auto' | 'staged' | 'fused' | 'bitsliced' | 'bitsliced6' | 'stream'.
+
+    `tile` selects a variant: 'bitsliced' lanes per column group (0, 1, 4), 'bitsliced6'
+    tile width (0 = 256 B, 4 = 128 B), 'stream' loader waves (0 = default 2, 1, 2, 4).
+    Every accepted path produces the reference's parity; anything else raises ValueError.
+    Returns the previous path name."""
+    if mode not in _ENCODE_PATHS:
+        raise ValueError(f"unknown encode path {mode!r}")
+    prev = _lib.lib().clay_set_encode_path(_ENCODE_PATHS[mode] | (int(tile) << 8))
+    if prev < 0:
+        raise ValueError(f"encode path {mode!r} has no variant {tile}")
+    return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
 def last_encode_path() -> str:

@@ -165,64 +165,21 @@ struct Map {
 };
 }  // namespace v6
 
-#ifdef CLAY_STAMPS
-__device__ uint64_t *g_clay_stamps;  // [block][wave][phase] cycle sums (tools/stamp_v6.hip)
-#define CLAY_ST(i)                                              \
-    do {                                                        \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();       \
-        st_acc[i] += t_ - st_prev;                              \
-        st_prev = t_;                                           \
-    } while (0)
-#else
-#define CLAY_ST(i) \
-    do {           \
-    } while (0)
-#endif
-
-// 16-byte store, SGPR base + per-lane 32-bit offset (one VMEM instruction, counted)
-__device__ __forceinline__ void st16s(const uint8_t *sbase, uint32_t voff, uint32_t a, uint32_t b, uint32_t c,
-                                      uint32_t d) {
-    const u32x4 v = {a, b, c, d};
-    // s_nop 1: hipcc does not pad an asm store's data hazard (the next instruction may
-    // overwrite the data VGPRs before the store has read them)
-    asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
-}
-// same with the non-temporal hint: parity is written once and never re-read by the kernel
-__device__ __forceinline__ void st16s_nt(const uint8_t *sbase, uint32_t voff, uint32_t a, uint32_t b, uint32_t c,
-                                         uint32_t d) {
-    const u32x4 v = {a, b, c, d};
-    asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field)
-__device__ __forceinline__ void wait_vm_rt(int n) {
-    switch (n < 63 ? n : 63) {
-#define CLAY_W1(k) case k: wait_vm_n<k>(); break;
-#define CLAY_W8(k) CLAY_W1(k) CLAY_W1(k + 1) CLAY_W1(k + 2) CLAY_W1(k + 3) CLAY_W1(k + 4) CLAY_W1(k + 5) CLAY_W1(k + 6) CLAY_W1(k + 7)
-        CLAY_W8(0) CLAY_W8(8) CLAY_W8(16) CLAY_W8(24) CLAY_W8(32) CLAY_W8(40) CLAY_W8(48) CLAY_W8(56)
-#undef CLAY_W8
-#undef CLAY_W1
-        default: wait_vm_n<0>(); break;
-    }
-}
-
-template <int KD, int M, int PARTS, bool EARLY, bool NTS = false>
+template <int KD, int M, int PARTS>
 struct Bs6Kernel {
     using S = Shape<KD, M>;
     using MP = v6::Map<PARTS>;
     static constexpr int PB = v6::Layout<PARTS>::PB;
     static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
-    static_assert(KD == 10 && M == 4 && Q == 4 && T == 4 && ALPHA == 256,
-                  "v6 slot layout is derived for (10,4,13)");
+    static_assert(M == 4 && Q == 4 && T == 4 && ALPHA == 256 && KD <= 12,
+                  "v6 slot layout is derived for q = 4, t = 4 (alpha 256)");
     static constexpr int W = 32 * PARTS, COLS = ALPHA / Q, BLOCK = COLS * PARTS, WAVES = BLOCK / 64;
     static constexpr int NODE_BYTES = COLS * W;            // one node of one (Y, g) slot
     static constexpr int SLOT = Q * NODE_BYTES;            // 32 KiB (W 128) / 64 KiB (W 256)
     static constexpr int RING = (160 * 1024) / SLOT;       // 5 / 2
     static constexpr int LDS_BYTES = RING * SLOT;
-    // slots in flight ahead of the one being read: with EARLY the step pulls its whole slot
-    // into registers and releases it at a second barrier, so the slot just read is refilled
-    // before the compute (RING slots in flight); otherwise it is refilled next step
-    static constexpr int AHEAD = EARLY ? RING : RING - 1;
+    // slots in flight ahead of the one being read (the slot just read is refilled next step)
+    static constexpr int AHEAD = RING - 1;
     static constexpr int STEPS = (T - 1) * Q;              // (section, group) steps per tile
     static constexpr int DMA_PER_NODE = NODE_BYTES / 1024 / WAVES;  // per wave: 2
 
@@ -407,25 +364,6 @@ struct Bs6Kernel {
             fold_x<Y, x>(u, acc);
         });
     }
-    // EARLY: all of the step's reads + PRT first (U: 32 VGPRs), then the caller
-    // releases the slot and folds.
-    template <int Y>
-    __device__ static void load_prt_all(const uint8_t *slot, const LaneC &L, uint32_t (&u)[Q][8]) {
-        sfor<Q>([&](auto xc) BS_INL {
-            constexpr int x = decltype(xc)::value;
-            uint32_t o[8], cv[8];
-            load_x<Y, x>(slot, L, o, cv);
-            prt_x<Y, x>(o, cv, L, u[x]);
-        });
-    }
-    template <int Y>
-    __device__ static void fold_all(uint32_t (&u)[Q][8], uint32_t (&acc)[Q * 8]) {
-        sfor<Q>([&](auto xc) BS_INL {
-            constexpr int x = decltype(xc)::value;
-            fold_x<Y, x>(u[x], acc);
-        });
-    }
-
     // Parity output C (8 planes) -> bytes -> HBM at parity node x, layer z.  Stores use
     // the SGPR-base + 32-bit offset form; the offset is formed here and kept opaque,
     // otherwise LICM hoists all 16 (node, layer) 64-bit addresses out of the tile loop.
@@ -436,13 +374,8 @@ struct Bs6Kernel {
         asm volatile("" : "+v"(off));
         off += pos;
         if (!ragged) {
-            if constexpr (NTS) {
-                st16s_nt(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
-                st16s_nt(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
-            } else {
-                st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
-                st16s(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
-            }
+            st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
+            st16s(a.par[X], off + 16u, cv[4], cv[5], cv[6], cv[7]);
         } else {
             uint8_t *p = a.par[X] + off;
 #pragma unroll
@@ -509,9 +442,9 @@ struct Bs6Kernel {
     }
 };
 
-template <int KD, int M, int PARTS, bool EARLY, bool NTS = false>
-__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void k_bs6_encode(BsArgs a) {
-    using Kn = Bs6Kernel<KD, M, PARTS, EARLY, NTS>;
+template <int KD, int M, int PARTS>
+__global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS>::BLOCK)) void k_bs6_encode(BsArgs a) {
+    using Kn = Bs6Kernel<KD, M, PARTS>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int c = int(threadIdx.x) >> Kn::PB, part = int(threadIdx.x) & (PARTS - 1);
@@ -542,9 +475,6 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void 
     typename Kn::Hold H;
     const typename Kn::LaneC L = Kn::lane_consts(c, part);
     const uint32_t sc = uint32_t(a.sc);
-#ifdef CLAY_STAMPS
-    uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
-#endif
     for (int s = 0; s < nsteps; s++) {
         const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
         const uint32_t b0 = tile_b0(k);
@@ -556,20 +486,8 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void 
         } else {
             wait_vm_rt(Tn - mk[0]);
         }
-        CLAY_ST(0);
         lds_barrier();
-        CLAY_ST(1);
-        if constexpr (EARLY) {
-            uint32_t u[Kn::Q][8];
-            if (y == 0) Kn::template load_prt_all<0>(slotp, L, u);
-            else if (y == 1) Kn::template load_prt_all<1>(slotp, L, u);
-            else Kn::template load_prt_all<2>(slotp, L, u);
-            lds_barrier();         // every wave holds its step in registers: the slot is free
-            issue(s + Kn::AHEAD);  // refill it with the slot AHEAD steps on
-            if (y == 0) Kn::template fold_all<0>(u, acc);
-            else if (y == 1) Kn::template fold_all<1>(u, acc);
-            else Kn::template fold_all<2>(u, acc);
-        } else {
+        {
             // refill the slot every wave finished reading last step, one node per x below
             const int s2 = s + Kn::AHEAD;
             const bool more = s2 < nsteps;
@@ -581,7 +499,6 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void 
                 constexpr int x = decltype(xc)::value;
                 if (more) Kn::template dma_node_any<x>(y2, a, slot2, wave, vl, nb0, g2);
             };
-            CLAY_ST(2);
             if (y == 0) Kn::template section<0>(slotp, L, acc, pre);
             else if (y == 1) Kn::template section<1>(slotp, L, acc, pre);
             else Kn::template section<2>(slotp, L, acc, pre);
@@ -590,7 +507,6 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void 
             for (int j = 0; j + 1 < Kn::AHEAD; j++) mk[j] = mk[j + 1];
             mk[Kn::AHEAD - 1] = Tn;
         }
-        CLAY_ST(3);
         if (y == 2) {
             const uint32_t pos = b0 + uint32_t(32 * part);
             const int nv = pos >= sc ? 0 : ((sc - pos) / 8 > 4 ? 4 : int((sc - pos) / 8));
@@ -600,17 +516,8 @@ __global__ __launch_bounds__((Bs6Kernel<KD, M, PARTS, EARLY, NTS>::BLOCK)) void 
             else Kn::template end_group<3>(a, acc, H, c, pos, ragged, nv);
             Tn += Kn::stores(g);
         }
-        CLAY_ST(4);
     }
     wait_vm0();
-#ifdef CLAY_STAMPS
-    CLAY_ST(5);
-    if (lane == 0) {
-        uint64_t *o = g_clay_stamps + (uint64_t(blockIdx.x) * Kn::WAVES + wave) * 8;
-        for (int i = 0; i < 6; i++) o[i] = st_acc[i];
-        o[6] = uint64_t(nsteps);
-    }
-#endif
 }
 
 }  // namespace bs

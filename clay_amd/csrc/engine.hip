@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -29,8 +30,7 @@
 #include "gf256.hpp"
 #include "bitslice.hpp"
 #include "bitslice6.hpp"
-#include "bitslice7.hpp"
-#include "bitslice8.hpp"
+#include "stream_encode.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -46,38 +46,6 @@ constexpr size_t kFusedLdsBudget = 128 * 1024;
 struct ExecPtrs {
     uint8_t *p[kMaxBases];
 };
-
-// ---------------------------------------------------------------------------
-// Generic staged executor: one workgroup = one op x one tile of positions.
-// dst[pos] = XOR_s coef_s * src_s[pos]  over the op's sources.
-// ---------------------------------------------------------------------------
-template <int VW>
-__global__ __launch_bounds__(kExecBlock) void k_exec(ExecPtrs P, const DevOp *__restrict__ ops,
-                                                     const DevSrc *__restrict__ srcs,
-                                                     const uint32_t *__restrict__ tabs, uint32_t op0,
-                                                     uint32_t tiles, uint64_t sc) {
-    constexpr int NW = (VW + 3) / 4;
-    const uint32_t opi = blockIdx.x / tiles, tile = blockIdx.x - opi * tiles;
-    const DevOp op = ops[op0 + opi];
-    const uint64_t pos = (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
-    if (pos >= sc) return;
-    Words<NW> acc;
-#pragma unroll
-    for (int w = 0; w < NW; w++) acc.w[w] = 0;
-    for (uint32_t s = 0; s < op.nsrc; ++s) {
-        const DevSrc d = srcs[op.src_begin + s];
-        const Words<NW> v = vload<VW>(P.p[d.base] + uint64_t(d.slot) * sc + pos);
-        if (d.coef == 1) {
-#pragma unroll
-            for (int w = 0; w < NW; w++) acc.w[w] ^= v.w[w];
-        } else {
-            const GfTab t = load_tab(tabs + d.coef * 8);
-#pragma unroll
-            for (int w = 0; w < NW; w++) acc.w[w] ^= gf_mul(v.w[w], t);
-        }
-    }
-    vstore<VW>(P.p[op.base] + uint64_t(op.slot) * sc + pos, acc);
-}
 
 // Grouped staged executor: one workgroup = one source-sharing op group x one tile.
 // Each source tile is loaded once, split into its perm-table indices once, and
@@ -189,123 +157,6 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
     }
 }
 
-
-// ---------------------------------------------------------------------------
-// Fused tile executor: the whole grouped plan per tile of W byte positions, U
-// plane and re-read intermediates in LDS (no workspace round trips through HBM).
-// A lane group of W/16 lanes runs one group (16 bytes per lane); all lane groups
-// of the workgroup sweep a level's groups, then a barrier separates levels --
-// the same read-before-write order as one launch per level.  LDS = GF perm
-// tables (256 x 8 dwords) + nslots x W bytes (slots reused across levels).
-// ---------------------------------------------------------------------------
-constexpr int kFxBlock = 512;
-constexpr int kFxBatch = 8;
-struct FxArgs {
-    const DevGroup *groups;
-    const DevSrc *srcs, *dsts;
-    const int32_t *src_lds, *dst_lds;  // LDS slot (-1: global source / no slot)
-    const uint32_t *dst_glb;          // 1: also store to the global region
-    const uint32_t *coef;
-    const uint2 *pcoef;               // per source: its coefficient for dst d in byte d (8 dsts max)
-    const uint32_t *tabs;
-    const uint32_t *stage_begin;
-    uint32_t nstages, W, ntiles, pad;
-    uint64_t sc;
-};
-
-template <int MAXD>
-__global__ __launch_bounds__(kFxBlock) void k_fexec(ExecPtrs P, FxArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t *ltab = reinterpret_cast<uint32_t *>(lds);
-    uint8_t *slots = lds + 256 * 8 * 4;
-    for (uint32_t i = threadIdx.x; i < 256 * 8; i += kFxBlock) ltab[i] = a.tabs[i];
-    const uint32_t LG = a.W / 16, nlg = kFxBlock / LG, lg = threadIdx.x / LG, li = threadIdx.x - lg * LG;
-    __syncthreads();
-    for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-        const uint64_t pos = uint64_t(tile) * a.W + uint64_t(li) * 16;
-        const uint32_t nb = pos >= a.sc ? 0u : uint32_t(a.sc - pos < 16 ? a.sc - pos : 16);
-        for (uint32_t st = 0; st < a.nstages; st++) {
-            const uint32_t gend = a.stage_begin[st + 1];
-            for (uint32_t gi = a.stage_begin[st] + lg; gi < gend; gi += nlg) {
-                const DevGroup g = a.groups[gi];
-                uint32_t acc[MAXD][4];
-#pragma unroll
-                for (int d = 0; d < MAXD; d++) acc[d][0] = acc[d][1] = acc[d][2] = acc[d][3] = 0;
-                // sources in batches of kFxBatch: every load of a batch is issued before
-                // the first multiply, so HBM latency is paid once per batch
-                for (uint32_t s0 = 0; s0 < g.nsrc; s0 += kFxBatch) {
-                    uint32_t v[kFxBatch][4];
-                    uint2 cb[kFxBatch];
-#pragma unroll
-                    for (int b = 0; b < kFxBatch; b++) {
-                        const uint32_t s = s0 + b;
-                        v[b][0] = v[b][1] = v[b][2] = v[b][3] = 0;
-                        cb[b] = make_uint2(0, 0);
-                        if (s < g.nsrc) {
-                            cb[b] = a.pcoef[g.src_begin + s];
-                            const int32_t sl = a.src_lds[g.src_begin + s];
-                            if (sl >= 0) {
-                                const uint4 x = *reinterpret_cast<const uint4 *>(slots + uint32_t(sl) * a.W + li * 16);
-                                v[b][0] = x.x; v[b][1] = x.y; v[b][2] = x.z; v[b][3] = x.w;
-                            } else {
-                                const DevSrc src = a.srcs[g.src_begin + s];
-                                const uint8_t *sp = P.p[src.base] + uint64_t(src.slot) * a.sc + pos;
-                                if (nb == 16) {
-                                    __builtin_memcpy(v[b], sp, 16);
-                                } else {
-                                    uint8_t tb[16] = {};
-                                    for (uint32_t i = 0; i < nb; i++) tb[i] = sp[i];
-                                    __builtin_memcpy(v[b], tb, 16);
-                                }
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int b = 0; b < kFxBatch; b++) {
-                        const uint32_t s = s0 + b;
-                        if (s >= g.nsrc) break;
-                        GfIdx ix[4];
-#pragma unroll
-                        for (int w = 0; w < 4; w++) ix[w] = gf_idx(v[b][w]);
-#pragma unroll
-                        for (int d = 0; d < MAXD; d++) {
-                            if (d >= int(g.ndst)) break;
-                            const uint32_t c = ((d < 4 ? cb[b].x : cb[b].y) >> (8 * (d & 3))) & 0xffu;
-                            if (c == 1) {
-#pragma unroll
-                                for (int w = 0; w < 4; w++) acc[d][w] ^= v[b][w];
-                            } else {
-                                const GfTab t = load_tab(ltab + c * 8);
-#pragma unroll
-                                for (int w = 0; w < 4; w++) acc[d][w] ^= gf_mul_idx(ix[w], t);
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int d = 0; d < MAXD; d++) {
-                    if (d >= int(g.ndst)) break;
-                    const int32_t dl = a.dst_lds[g.dst_begin + d];
-                    if (dl >= 0)
-                        *reinterpret_cast<uint4 *>(slots + uint32_t(dl) * a.W + li * 16) =
-                            make_uint4(acc[d][0], acc[d][1], acc[d][2], acc[d][3]);
-                    if (a.dst_glb[g.dst_begin + d] && nb) {
-                        const DevSrc dst = a.dsts[g.dst_begin + d];
-                        uint8_t *dp = P.p[dst.base] + uint64_t(dst.slot) * a.sc + pos;
-                        if (nb == 16) {
-                            __builtin_memcpy(dp, acc[d], 16);
-                        } else {
-                            uint8_t tb[16];
-                            __builtin_memcpy(tb, acc[d], 16);
-                            for (uint32_t i = 0; i < nb; i++) dp[i] = tb[i];
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Fused encode (parity = last y-section).  See file header and DESIGN.md.
@@ -469,8 +320,27 @@ __global__ __launch_bounds__(kFusedBlock) void k_fused_encode(FusedArgs a, const
 static std::mutex g_mu;
 static thread_local std::string t_last_path = "none";
 static thread_local size_t t_last_launches = 0;
-static int g_encode_mode = 0;
-static int g_bs_pg = 0;  // bit-sliced tile width override (lanes of 32 positions); 0 = default
+// Encode path selection (clay_set_encode_path): process-wide, read without locks.
+enum : int { kModeAuto = 0, kModeStaged = 1, kModeFused = 2, kModeBs = 3, kModeBs6 = 4, kModeStream = 5 };
+static std::atomic<int> g_encode_mode{kModeAuto};
+static std::atomic<int> g_encode_tile{0};  // per-mode variant (see clay_set_encode_path)
+
+// Device properties the launchers need, queried once per device.
+struct DevProps {
+    int dev = 0;
+    int cus = 256;
+    hipDeviceProp_t raw{};
+};
+static DevProps g_props[64];
+static std::once_flag g_props_once[64];
+static const DevProps &dev_props(int dev) {
+    std::call_once(g_props_once[dev], [dev] {
+        DevProps &p = g_props[dev];
+        p.dev = dev;
+        if (hipGetDeviceProperties(&p.raw, dev) == hipSuccess) p.cus = p.raw.multiProcessorCount;
+    });
+    return g_props[dev];
+}
 
 struct Workspace {
     void *ptr = nullptr;
@@ -492,27 +362,17 @@ struct DevState {
 };
 static DevState g_dev[64];
 
-// Fused-tile program for a plan (built once per plan, per device).
-struct FxProg {
-    bool ok = false;
-    uint32_t W = 0, nslots = 0, maxd = 1;
-    size_t lds = 0;
-    FxArgs dev{};
-};
-
 struct CodeState {
     clay_code_t code{};
     RsCtx rs;
     std::unique_ptr<Plan> enc;
     std::map<std::vector<uint8_t>, std::unique_ptr<Plan>> dec, rep;
-    std::map<std::pair<const Plan *, int>, std::pair<void *, void *>> dplan;
     struct DevGrouped {
         const DevGroup *groups;
         const DevSrc *srcs, *dsts;
         const uint32_t *coef;
     };
     std::map<std::pair<const Plan *, int>, DevGrouped> gplan;
-    std::map<std::pair<const Plan *, int>, FxProg> fplan;
     std::map<int, uint32_t *> mtab;
     explicit CodeState(const clay_code_t &c) : code(c), rs(c) {}
 };
@@ -570,23 +430,6 @@ static CodeState *code_state(const clay_code_t &c) {
     return p;
 }
 
-static Error upload_plan(CodeState &cs, const Plan &pl, int dev, const DevOp **ops, const DevSrc **srcs) {
-    auto key = std::make_pair(&pl, dev);
-    auto it = cs.dplan.find(key);
-    if (it == cs.dplan.end()) {
-        void *o = nullptr, *s = nullptr;
-        CLAY_HIP(hipMalloc(&o, std::max<size_t>(1, pl.ops.size()) * sizeof(DevOp)));
-        CLAY_HIP(hipMalloc(&s, std::max<size_t>(1, pl.srcs.size()) * sizeof(DevSrc)));
-        if (!pl.ops.empty()) CLAY_HIP(hipMemcpy(o, pl.ops.data(), pl.ops.size() * sizeof(DevOp), hipMemcpyHostToDevice));
-        if (!pl.srcs.empty())
-            CLAY_HIP(hipMemcpy(s, pl.srcs.data(), pl.srcs.size() * sizeof(DevSrc), hipMemcpyHostToDevice));
-        it = cs.dplan.emplace(key, std::make_pair(o, s)).first;
-    }
-    *ops = static_cast<const DevOp *>(it->second.first);
-    *srcs = static_cast<const DevSrc *>(it->second.second);
-    return Error{};
-}
-
 template <typename T>
 static Error upload_vec(const std::vector<T> &v, const T **out) {
     void *p = nullptr;
@@ -636,157 +479,6 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
 }
 
 
-static constexpr size_t kFxLdsCap = 150 * 1024;
-
-static void build_fx(const Plan &pl, FxProg &fx, std::vector<int32_t> &src_lds, std::vector<int32_t> &dst_lds,
-                     std::vector<uint32_t> &dst_glb) {
-    const size_t ns = pl.gstage_begin.size() - 1;
-    const uint32_t ubase = 2 * pl.tn;
-    auto rk = [](const DevSrc &d) { return (uint64_t(d.base) << 32) | d.slot; };
-    std::map<uint64_t, int> first_w, last_use;
-    for (size_t st = 0; st < ns; st++)
-        for (uint32_t gi = pl.gstage_begin[st]; gi < pl.gstage_begin[st + 1]; gi++) {
-            const DevGroup &g = pl.groups[gi];
-            for (uint32_t d = 0; d < g.ndst; d++) {
-                uint64_t r = rk(pl.gdsts[g.dst_begin + d]);
-                if (!first_w.count(r)) first_w[r] = int(st);
-                last_use[r] = std::max(last_use.count(r) ? last_use[r] : 0, int(st));
-            }
-        }
-    std::map<uint64_t, bool> read_after;
-    for (size_t st = 0; st < ns; st++)
-        for (uint32_t gi = pl.gstage_begin[st]; gi < pl.gstage_begin[st + 1]; gi++) {
-            const DevGroup &g = pl.groups[gi];
-            for (uint32_t s = 0; s < g.nsrc; s++) {
-                uint64_t r = rk(pl.gsrcs[g.src_begin + s]);
-                auto it = first_w.find(r);
-                if (it == first_w.end()) continue;
-                if (it->second >= int(st)) return;  // read before its first write: not expressible
-                read_after[r] = true;
-                last_use[r] = std::max(last_use[r], int(st));
-            }
-        }
-    // interval colouring of the regions that are read back: [first write, last use]
-    std::vector<std::pair<int, uint64_t>> order;
-    for (auto &kv : first_w)
-        if (read_after.count(kv.first)) order.push_back({kv.second, kv.first});
-    std::sort(order.begin(), order.end());
-    std::vector<int> slot_end;  // per slot: last level it is busy
-    std::map<uint64_t, int32_t> slot_of;
-    for (auto &o : order) {
-        int sl = -1;
-        for (size_t i = 0; i < slot_end.size(); i++)
-            if (slot_end[i] < o.first) { sl = int(i); break; }
-        if (sl < 0) { sl = int(slot_end.size()); slot_end.push_back(0); }
-        slot_end[sl] = last_use[o.second];
-        slot_of[o.second] = sl;
-    }
-    fx.nslots = uint32_t(slot_end.size());
-    // widest tile that still lets 2 workgroups share a CU, else the widest that fits
-    for (size_t cap : {size_t(64 * 1024), kFxLdsCap}) {
-        for (uint32_t W : {2048u, 1024u, 512u, 256u, 128u, 64u}) {
-            size_t need = 256 * 8 * 4 + size_t(fx.nslots) * W;
-            if (need <= cap) { fx.W = W; fx.lds = need; break; }
-        }
-        if (fx.W) break;
-    }
-    if (!fx.W) return;
-    src_lds.resize(pl.gsrcs.size());
-    for (size_t i = 0; i < pl.gsrcs.size(); i++) {
-        auto it = slot_of.find(rk(pl.gsrcs[i]));
-        src_lds[i] = it == slot_of.end() ? -1 : it->second;
-        if (it == slot_of.end() && first_w.count(rk(pl.gsrcs[i]))) return;
-    }
-    dst_lds.resize(pl.gdsts.size());
-    dst_glb.resize(pl.gdsts.size());
-    for (size_t i = 0; i < pl.gdsts.size(); i++) {
-        auto it = slot_of.find(rk(pl.gdsts[i]));
-        dst_lds[i] = it == slot_of.end() ? -1 : it->second;
-        dst_glb[i] = pl.gdsts[i].base != ubase;  // U never leaves the chip; C / OUT regions always written
-    }
-    for (uint32_t m : pl.gstage_maxd) fx.maxd = std::max(fx.maxd, m);
-    fx.ok = true;
-}
-
-// Executor for plans: 0 = k_exec (one op per block), 1 = k_gexec grouped (default),
-// 2 = k_fexec fused tile executor when the plan fits LDS.  Initial value from
-// CLAY_EXEC ("ops" | "grouped" | "fused"); clay_set_exec_mode() overrides.
-static int g_exec_mode = [] {
-    const char *e = getenv("CLAY_EXEC");
-    return !e ? 1 : std::strcmp(e, "ops") == 0 ? 0 : std::strcmp(e, "fused") == 0 ? 2 : 1;
-}();
-static int exec_mode() { return g_exec_mode; }
-
-static Error run_fused(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
-                       const ExecPtrs &ptrs, size_t sc, bool *done) {
-    *done = false;
-    auto key = std::make_pair(&pl, dev);
-    auto it = cs.fplan.find(key);
-    if (it == cs.fplan.end()) {
-        FxProg fx;
-        std::vector<int32_t> sl, dl;
-        std::vector<uint32_t> dg;
-        build_fx(pl, fx, sl, dl, dg);
-        if (fx.ok) {
-            std::vector<uint2> pc(pl.gsrcs.size(), uint2{0, 0});
-            for (const DevGroup &gr : pl.groups)
-                for (uint32_t si = 0; si < gr.nsrc; si++)
-                    for (uint32_t d = 0; d < gr.ndst && d < 8; d++) {
-                        uint32_t c = pl.gcoef[gr.coef_begin + d * gr.nsrc + si] & 0xffu;
-                        if (d < 4) pc[gr.src_begin + si].x |= c << (8 * d);
-                        else pc[gr.src_begin + si].y |= c << (8 * (d - 4));
-                    }
-            const uint2 *dpc;
-            Error e0 = upload_vec(pc, &dpc);
-            if (e0) return e0;
-            fx.dev.pcoef = dpc;
-            CodeState::DevGrouped g{};
-            Error e = upload_groups(cs, pl, dev, &g);
-            if (e) return e;
-            const int32_t *dsl, *ddl;
-            const uint32_t *ddg, *dstb;
-            if ((e = upload_vec(sl, &dsl)) || (e = upload_vec(dl, &ddl)) || (e = upload_vec(dg, &ddg)) ||
-                (e = upload_vec(pl.gstage_begin, &dstb)))
-                return e;
-            fx.dev.groups = g.groups;
-            fx.dev.srcs = g.srcs;
-            fx.dev.dsts = g.dsts;
-            fx.dev.coef = g.coef;
-            fx.dev.src_lds = dsl;
-            fx.dev.dst_lds = ddl;
-            fx.dev.dst_glb = ddg;
-            fx.dev.stage_begin = dstb;
-            fx.dev.nstages = uint32_t(pl.gstage_begin.size() - 1);
-        }
-        if (getenv("CLAY_FX_DEBUG"))
-            fprintf(stderr, "[clay fx] ok=%d W=%u slots=%u lds=%zu maxd=%u stages=%zu groups=%zu\n", int(fx.ok), fx.W,
-                    fx.nslots, fx.lds, fx.maxd, pl.gstage_begin.size() - 1, pl.groups.size());
-        it = cs.fplan.emplace(key, fx).first;
-    }
-    FxProg &fx = it->second;
-    if (!fx.ok) return Error{};
-    FxArgs a = fx.dev;
-    a.tabs = ds.d_tabs;
-    a.W = fx.W;
-    a.sc = sc;
-    a.ntiles = uint32_t((sc + fx.W - 1) / fx.W);
-    const int per_cu = fx.lds <= 64 * 1024 ? 2 : 1;
-    const uint32_t grid = std::min<uint32_t>(a.ntiles, uint32_t(256 * per_cu * (1024 / kFxBlock)));
-    auto launch = [&](auto kern) -> Error {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     int(kFxLdsCap)));
-        kern<<<dim3(grid), dim3(kFxBlock), fx.lds, stream>>>(ptrs, a);
-        CLAY_HIP(hipGetLastError());
-        return Error{};
-    };
-    Error e = fx.maxd <= 1 ? launch(k_fexec<1>) : fx.maxd <= 2 ? launch(k_fexec<2>)
-            : fx.maxd <= 4 ? launch(k_fexec<4>) : launch(k_fexec<8>);
-    if (e) return e;
-    t_last_launches += 1;
-    *done = true;
-    return Error{};
-}
-
 static Error ensure_ws(DevState &ds, void *stream, size_t bytes, void **out) {
     Workspace &w = ds.ws[stream];
     if (w.bytes < bytes) {
@@ -809,77 +501,31 @@ static int align_of(uintptr_t p) {
     return 1;
 }
 
-// Execute a plan: C/H/OUT pointer bindings given, U workspace bound here.
+// Execute a plan: C/H/OUT pointer bindings given, U workspace bound here.  One k_gexec
+// launch per dependency level; 16 bytes per lane regardless of sc / pointer alignment.
 static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
                       ExecPtrs ptrs, size_t sc, size_t chunk_for_ws) {
-    const DevOp *d_ops;
-    const DevSrc *d_srcs;
-    Error e = upload_plan(cs, pl, dev, &d_ops, &d_srcs);
-    if (e) return e;
-    if (exec_mode() == 2 && pl.gstage_begin.size() == pl.stage_begin.size()) {
-        bool done = false;
-        e = run_fused(cs, pl, dev, ds, stream, ptrs, sc, &done);
-        if (e || done) return e;
-    }
+    Error e;
     if (pl.uses_u) {
         void *ws = nullptr;
         e = ensure_ws(ds, stream, size_t(pl.tn) * chunk_for_ws, &ws);
         if (e) return e;
         ptrs.p[2 * pl.tn] = static_cast<uint8_t *>(ws);
     }
-    int vw = 16;
-    while (vw > 1 && (sc % vw) != 0) vw >>= 1;
-    for (int i = 0; i < kMaxBases; i++)
-        if (ptrs.p[i]) vw = std::min(vw, align_of(reinterpret_cast<uintptr_t>(ptrs.p[i])));
-    const uint64_t per_thread = uint64_t(vw);
-    const uint32_t tiles = uint32_t((sc / per_thread + kExecBlock - 1) / kExecBlock);
+    CodeState::DevGrouped g{};
+    e = upload_groups(cs, pl, dev, &g);
+    if (e) return e;
     size_t launches = 0;
-    if (exec_mode() >= 1 && pl.gstage_begin.size() == pl.stage_begin.size()) {
-        // 16 bytes per lane regardless of sc / pointer alignment (see k_gexec).
-        // CLAY_EXEC_RANGE=B runs all stages over byte range [r0, r0+B) of every
-        // sub-chunk before the next range (cache-resident U round trips).
-        static const uint64_t range_env = [] {
-            const char *e = getenv("CLAY_EXEC_RANGE");
-            return e ? uint64_t(strtoull(e, nullptr, 10)) / 16 * 16 : uint64_t(0);
-        }();
-        const uint64_t range = range_env ? range_env : sc;
-        CodeState::DevGrouped g{};
-        e = upload_groups(cs, pl, dev, &g);
-        if (e) return e;
-        for (uint64_t r0 = 0; r0 < sc; r0 += range) {
-            const uint64_t r1 = std::min<uint64_t>(sc, r0 + range);
-            const uint32_t tiles = uint32_t(((r1 - r0) / 16 + 1 + kExecBlock - 1) / kExecBlock);
-            for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
-                uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
-                const uint32_t maxd = pl.gstage_maxd[s];
-                while (b < end) {
-                    uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
-                    dim3 grid(n * tiles);
-                    launch_gexec<16>(maxd, grid, stream, ptrs, g, ds.d_tabs, b, tiles, sc, r0, r1, n);
-                    CLAY_HIP(hipGetLastError());
-                    launches++;
-                    b += n;
-                }
-            }
-        }
-        t_last_launches += launches;
-        return Error{};
-    }
-    for (size_t s = 0; s + 1 < pl.stage_begin.size(); s++) {
-        uint32_t b = pl.stage_begin[s], end = pl.stage_begin[s + 1];
+    const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+    for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
+        uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
+        const uint32_t maxd = pl.gstage_maxd[s];
         while (b < end) {
-            uint32_t nops = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
-            dim3 grid(nops * tiles), block(kExecBlock);
-            switch (vw) {
-            case 16: k_exec<16><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
-            case 8: k_exec<8><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
-            case 4: k_exec<4><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
-            case 2: k_exec<2><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
-            default: k_exec<1><<<grid, block, 0, stream>>>(ptrs, d_ops, d_srcs, ds.d_tabs, b, tiles, sc); break;
-            }
+            uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
+            launch_gexec<16>(maxd, dim3(n * tiles), stream, ptrs, g, ds.d_tabs, b, tiles, sc, 0, sc, n);
             CLAY_HIP(hipGetLastError());
             launches++;
-            b += nops;
+            b += n;
         }
     }
     t_last_launches += launches;
@@ -934,8 +580,7 @@ static Error encode_fused(CodeState &cs, DevState &ds, int dev, const uint8_t *c
         CLAY_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
         it = cs.mtab.emplace(dev, d).first;
     }
-    hipDeviceProp_t prop;
-    CLAY_HIP(hipGetDeviceProperties(&prop, dev));
+    const hipDeviceProp_t &prop = dev_props(dev).raw;
     const size_t lds = Q * alpha * W;
     const int per_cu = std::max<int>(1, int((160 * 1024) / lds));
     for (size_t s = 0; s < n_stripes; s++) {
@@ -1014,136 +659,10 @@ static Error launch_bs(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t
     return Error{};
 }
 
-template <int KD, int M>
-static Error launch_bs2(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs2Kernel<KD, M>;
-    using S = typename Kn::S;
-    const clay_code_t &c = cs.code;
-    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
-    // per-lane DMA offsets are 32-bit: (q-1) * q^(t-2) * sc + sc must fit
-    if (double(M - 1) * double(S::ALPHA / M) * double(sc) + double(sc) >= 4294967296.0) return Error{};
-    for (int p = 0; p < M; p++)
-        for (int i = 0; i < S::K; i++)
-            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
-                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs2_encode<KD, M>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
-    }
-    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
-    for (size_t s = 0; s < n_stripes; s++) {
-        bs::BsArgs a{};
-        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
-        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
-        a.sc = sc;
-        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
-        a.tiles_per_xcd = (a.ntiles + 7) / 8;
-        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
-        a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs2_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
-        CLAY_HIP(hipGetLastError());
-        t_last_launches++;
-    }
-    char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced2-k%dm%d-w%d", KD, M, Kn::W);
-    t_last_path = buf;
-    *done = true;
-    return Error{};
-}
-
-template <int KD, int M>
-static Error launch_bs4(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs4Kernel<KD, M>;
-    using S = typename Kn::S;
-    const clay_code_t &c = cs.code;
-    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
-    // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 64
-    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 64) return Error{};
-    for (int p = 0; p < M; p++)
-        for (int i = 0; i < S::K; i++)
-            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
-                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs4_encode<KD, M>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
-    }
-    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
-    for (size_t s = 0; s < n_stripes; s++) {
-        bs::BsArgs a{};
-        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
-        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
-        a.sc = sc;
-        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
-        a.tiles_per_xcd = (a.ntiles + 7) / 8;
-        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
-        a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs4_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
-        CLAY_HIP(hipGetLastError());
-        t_last_launches++;
-    }
-    char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced4-k%dm%d-w%d", KD, M, Kn::W);
-    t_last_path = buf;
-    *done = true;
-    return Error{};
-}
-
-template <int KD, int M>
-static Error launch_bs5(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs5Kernel<KD, M>;
-    using S = typename Kn::S;
-    const clay_code_t &c = cs.code;
-    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
-    // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 64
-    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 64) return Error{};
-    for (int p = 0; p < M; p++)
-        for (int i = 0; i < S::K; i++)
-            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
-                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs5_encode<KD, M>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
-    }
-    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
-    for (size_t s = 0; s < n_stripes; s++) {
-        bs::BsArgs a{};
-        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
-        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
-        a.sc = sc;
-        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
-        a.tiles_per_xcd = (a.ntiles + 7) / 8;
-        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
-        a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs5_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
-        CLAY_HIP(hipGetLastError());
-        t_last_launches++;
-    }
-    char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced5-k%dm%d-w%d", KD, M, Kn::W);
-    t_last_path = buf;
-    *done = true;
-    return Error{};
-}
-
-template <int KD, int M, int PARTS, bool EARLY, bool NTS = false>
+template <int KD, int M, int PARTS>
 static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
                         size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs6Kernel<KD, M, PARTS, EARLY, NTS>;
+    using Kn = bs::Bs6Kernel<KD, M, PARTS>;
     using S = typename Kn::S;
     const clay_code_t &c = cs.code;
     if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
@@ -1157,7 +676,7 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
     int dev = 0;
     CLAY_HIP(hipGetDevice(&dev));
     if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS, EARLY, NTS>),
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
         attr[dev] = true;
     }
@@ -1171,24 +690,25 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
         a.tiles_per_xcd = (a.ntiles + 7) / 8;
         const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
         a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs6_encode<KD, M, PARTS, EARLY, NTS><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        bs::k_bs6_encode<KD, M, PARTS><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
         CLAY_HIP(hipGetLastError());
         t_last_launches++;
     }
     char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced6-k%dm%d-w%d%s%s", KD, M, Kn::W, EARLY ? "e" : "", NTS ? "-nts" : "");
+    std::snprintf(buf, sizeof(buf), "bitsliced6-k%dm%d-w%d", KD, M, Kn::W);
     t_last_path = buf;
     *done = true;
     return Error{};
 }
 
-template <bool NT, int PROBE = 0>
-static Error launch_bs7(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs7Kernel<NT>;
-    using S = typename Kn::K6::S;
+// The streaming encode (stream_encode.hpp) for q = 4, t = 4 codes with k = 9 or 10.
+template <int KD, int LOADERS>
+static Error launch_stream(CodeState &cs, const DevProps &prop, const uint8_t *const *data, uint8_t *const *par,
+                           size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::StreamEnc<KD, LOADERS>;
+    using S = typename Kn::S;
     const clay_code_t &c = cs.code;
-    if (c.k != 10 || c.m != 4 || c.d != 13) return Error{};
+    if (int(c.k) != KD || c.m != 4 || c.d != c.k + 3) return Error{};
     // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 16
     if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 16) return Error{};
     for (int p = 0; p < 4; p++)
@@ -1196,119 +716,36 @@ static Error launch_bs7(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
             if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
                 return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
     static bool attr[64] = {};
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs7_encode<NT, PROBE>),
+    if (!attr[prop.dev]) {
+        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_encode<KD, LOADERS>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
+        attr[prop.dev] = true;
     }
-    // XCD region: sc / 8 rounded up to 32 bytes; one 160 KiB workgroup per CU
+    // XCD region: sc / 8 rounded up to 32 bytes; one workgroup per CU
     const uint32_t region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
-    const uint32_t per_xcd = uint32_t(std::max(1, prop.multiProcessorCount / 8));
+    const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
     const uint32_t nslots = std::min(per_xcd, std::max(1u, (region + 255u) / 256u));
-    for (size_t s = 0; s < n_stripes; s++) {
-        bs::BsArgs a{};
-        for (int i = 0; i < S::K; i++) a.data[i] = i < 10 ? data[s * 10 + i] : nullptr;
-        for (int x = 0; x < 4; x++) a.par[x] = par[s * 4 + x];
-        a.sc = sc;
-        a.tiles_per_xcd = region;
-        a.nslots = nslots;
-        a.ntiles = 0;
-        bs::k_bs7_encode<NT, PROBE><<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
-        CLAY_HIP(hipGetLastError());
-        t_last_launches++;
-    }
-    t_last_path = NT ? "bitsliced7-k10m4-w256-nt" : "bitsliced7-k10m4-w256";
-    *done = true;
-    return Error{};
-}
-
-static Error launch_bs8(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs8Kernel;
-    using S = typename Kn::S;
-    const clay_code_t &c = cs.code;
-    if (c.k != 10 || c.m != 4 || c.d != 13) return Error{};
-    // per-lane offsets are 32-bit chunk offsets
-    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 16) return Error{};
-    for (int p = 0; p < 4; p++)
-        for (int i = 0; i < S::K; i++)
-            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
-                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs8_encode),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
-    }
-    // XCD region: sc / 8 rounded up to 32 bytes (TileMap7); one workgroup per CU
-    const uint32_t region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
-    const uint32_t per_xcd = uint32_t(std::max(1, prop.multiProcessorCount / 8));
-    const uint32_t nslots = std::min(per_xcd, std::max(1u, (region + 255u) / 256u));
-    for (size_t s = 0; s < n_stripes; s++) {
-        bs::BsArgs a{};
-        for (int i = 0; i < S::K; i++) a.data[i] = i < 10 ? data[s * 10 + i] : nullptr;
-        for (int x = 0; x < 4; x++) a.par[x] = par[s * 4 + x];
-        a.sc = sc;
-        a.tiles_per_xcd = region;
-        a.nslots = nslots;
-        a.ntiles = 0;
-        bs::k_bs8_encode<<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
-        CLAY_HIP(hipGetLastError());
-        t_last_launches++;
-    }
-    t_last_path = "bitsliced8-k10m4-w256";
-    *done = true;
-    return Error{};
-}
-
-template <int KD, int M>
-static Error launch_bs3(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs3Kernel<KD, M>;
-    using S = typename Kn::S;
-    const clay_code_t &c = cs.code;
-    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
-    // per-lane DMA offsets are 32-bit: 3 * sc + 64 must fit
-    if (double(sc) * 4.0 >= 4294967296.0) return Error{};
-    for (int p = 0; p < M; p++)
-        for (int i = 0; i < S::K; i++)
-            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
-                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs3_encode<KD, M>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
-    }
-    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
     for (size_t s = 0; s < n_stripes; s++) {
         bs::BsArgs a{};
         for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
-        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
+        for (int x = 0; x < 4; x++) a.par[x] = par[s * 4 + x];
         a.sc = sc;
-        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
-        a.tiles_per_xcd = (a.ntiles + 7) / 8;
-        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
-        a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs3_encode<KD, M><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        a.tiles_per_xcd = region;
+        a.nslots = nslots;
+        a.ntiles = 0;
+        bs::k_stream_encode<KD, LOADERS><<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
         CLAY_HIP(hipGetLastError());
         t_last_launches++;
     }
     char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced3-k%dm%d-w%d", KD, M, Kn::W);
+    std::snprintf(buf, sizeof(buf), "stream-k%dm4-w256-l%d", KD, LOADERS);
     t_last_path = buf;
     *done = true;
     return Error{};
 }
 
 static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data, uint8_t *const *par,
-                              size_t n_stripes, size_t chunk, hipStream_t stream, bool *done) {
+                              size_t n_stripes, size_t chunk, hipStream_t stream, int mode, int tile, bool *done) {
     *done = false;
     const clay_code_t &c = cs.code;
     const size_t sc = chunk / c.sub_chunk_no;
@@ -1319,76 +756,41 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
         for (size_t i = 0; i < c.m; i++)
             if (reinterpret_cast<uintptr_t>(par[s * c.m + i]) % 8) return Error{};
     }
-    hipDeviceProp_t prop;
-    CLAY_HIP(hipGetDeviceProperties(&prop, dev));
+    const DevProps &prop = dev_props(dev);
     Error e;
     const int key = int(c.k * 100 + c.m);
-    // v8 (register-staged loads three steps deep, plane exchange through LDS)
-    if (g_encode_mode == 10) {
-        if (key == 1004) e = launch_bs8(cs, prop, data, par, n_stripes, sc, stream, done);
-        if (e || *done || g_encode_mode == 10) return e;
-    }
-    // v7 (v6 compute, per-node LDS map with two steps in flight, balanced tail); tile
-    // override 1 = non-temporal DMA loads
-    if (g_encode_mode == 9) {
-        if (key == 1004) {
-            // override: 1 = nt loads; probes (wrong bytes): 2 memory-only, 4 compute-only,
-            // 6 reads-only, 10 memory-only without barriers, 14 reads-only without barriers
-            switch (g_bs_pg) {
-            case 1: e = launch_bs7<true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 2: e = launch_bs7<false, 1>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 4: e = launch_bs7<false, 2>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 6: e = launch_bs7<false, 5>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 10: e = launch_bs7<false, 9>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 14: e = launch_bs7<false, 13>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            default: e = launch_bs7<false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            }
+    // streaming kernel (q = 4, t = 4, k 9 / 10): auto's first choice; tile = loader waves
+    if (mode == kModeStream || mode == kModeAuto) {
+        if (key == 1004 || key == 904) {
+            const int l = tile ? tile : 4;
+            if (key == 1004)
+                e = l == 1 ? launch_stream<10, 1>(cs, prop, data, par, n_stripes, sc, stream, done)
+                  : l == 4 ? launch_stream<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done)
+                           : launch_stream<10, 2>(cs, prop, data, par, n_stripes, sc, stream, done);
+            else
+                e = launch_stream<9, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
         }
-        if (e || *done || g_encode_mode == 9) return e;
+        if (e || *done || mode == kModeStream) return e;
     }
-    // v6 (column-per-lane, PFT without exchange): 256-byte tiles / 2-slot ring by default
-    // (auto's first choice for (10,4,13)); tile override 4 = 128-byte tiles / 5-slot ring
-    if (g_encode_mode == 8 || (g_encode_mode == 0 && g_bs_pg == 0)) {
+    // v6 (column-per-lane, 2-slot ring); tile 4 = 128-byte tiles / 5-slot ring
+    if (mode == kModeBs6) {
         if (key == 1004) {
-            // tile override: 4 / 8 parts (128 / 256-byte tiles), +16 = early slot release,
-            // 40 = 256-byte tiles with non-temporal parity stores
-            switch (g_bs_pg) {
-            case 4: e = launch_bs6<10, 4, 4, false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 20: e = launch_bs6<10, 4, 4, true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 24: e = launch_bs6<10, 4, 8, true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            case 40: e = launch_bs6<10, 4, 8, false, true>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            default: e = launch_bs6<10, 4, 8, false>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-            }
+            if (tile == 4) e = launch_bs6<10, 4, 4>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
+            else e = launch_bs6<10, 4, 8>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
         }
-        if (e || *done || g_encode_mode == 8) return e;
+        return e;
     }
-    if (g_encode_mode == 7) {  // v5 (register accumulators, node-slot ring)
-        if (key == 1004) e = launch_bs5<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
-        if (e || *done || g_encode_mode == 7) return e;
-    }
-    if (g_encode_mode == 6 || (g_encode_mode == 0 && g_bs_pg == 0)) {  // v4 (16-byte LDS-DMA, conflict-free stage / accumulator)
-        if (key == 1004) e = launch_bs4<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
-        if (e || *done || g_encode_mode == 6) return e;
-    }
-    if (g_encode_mode == 5) {  // v3 (register accumulators, 2-slot ring)
-        if (key == 1004) e = launch_bs3<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
-        if (e || *done || g_encode_mode == 5) return e;
-    }
-    if (g_encode_mode != 3 && (g_bs_pg == 0 || g_encode_mode == 4)) {  // v2 (LDS-DMA staged)
-        if (key == 1004) e = launch_bs2<10, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
-        else if (key == 804) e = launch_bs2<8, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
-        if (e || *done || g_encode_mode == 4) return e;
-    }
+    // v1 (register loads, PG x 32 positions per lane): every q = m code it is instantiated for
     switch (key) {
     case 1004:
-        if (g_bs_pg == 1) e = launch_bs<10, 4, 1>(cs, prop, data, par, n_stripes, sc, stream, done);
-        else if (g_bs_pg == 4) e = launch_bs<10, 4, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
-        else e = launch_bs<10, 4, 2>(cs, prop, data, par, n_stripes, sc, stream, done);
+        if (tile == 1) e = launch_bs<10, 4, 1>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
+        else if (tile == 4) e = launch_bs<10, 4, 4>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
+        else e = launch_bs<10, 4, 2>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
         break;
-    case 402: e = launch_bs<4, 2, 64>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-    case 804: e = launch_bs<8, 4, 8>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-    case 903: e = launch_bs<9, 3, 6>(cs, prop, data, par, n_stripes, sc, stream, done); break;
-    case 603: e = launch_bs<6, 3, 16>(cs, prop, data, par, n_stripes, sc, stream, done); break;
+    case 402: e = launch_bs<4, 2, 64>(cs, prop.raw, data, par, n_stripes, sc, stream, done); break;
+    case 804: e = launch_bs<8, 4, 8>(cs, prop.raw, data, par, n_stripes, sc, stream, done); break;
+    case 903: e = launch_bs<9, 3, 6>(cs, prop.raw, data, par, n_stripes, sc, stream, done); break;
+    case 603: e = launch_bs<6, 3, 16>(cs, prop.raw, data, par, n_stripes, sc, stream, done); break;
     default: break;
     }
     return e;
@@ -1497,23 +899,24 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
         return make_error(CLAY_ERR_RECONSTRUCTION_FAILED, 0, 0, 0, "RS reconstruction failed: RS init failed: %s",
                           rs_error_name(cs.rs.init_err));
     hipStream_t st = static_cast<hipStream_t>(stream);
+    const int mode = g_encode_mode.load(std::memory_order_relaxed), tile = g_encode_tile.load(std::memory_order_relaxed);
     // many small stripes: one launch per plan level for the whole batch instead of
     // one launch per stripe (launch-bound below ~4 MiB of data per stripe)
-    if (g_encode_mode == 0 && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) && n_stripes <= 65535 &&
+    if (mode == kModeAuto && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) && n_stripes <= 65535 &&
         code->q * code->t <= size_t(kMaxTn))
         return encode_staged_batch(cs, *ds, dev, data, par, n_stripes, chunk, st);
-    if (g_encode_mode == 0 || g_encode_mode >= 3) {
+    if (mode == kModeAuto || mode >= kModeBs) {
         bool done = false;
-        e = encode_bitsliced(cs, dev, data, par, n_stripes, chunk, st, &done);
+        e = encode_bitsliced(cs, dev, data, par, n_stripes, chunk, st, mode, tile, &done);
         if (e || done) return e;
-        if (g_encode_mode >= 3)
+        if (mode >= kModeBs)
             return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced encode kernel does not support this code/alignment");
     }
-    if (g_encode_mode == 0 || g_encode_mode == 2) {
+    if (mode == kModeAuto || mode == kModeFused) {
         bool done = false;
         e = encode_fused(cs, *ds, dev, data, par, n_stripes, chunk, st, &done);
         if (e || done) return e;
-        if (g_encode_mode == 2)
+        if (mode == kModeFused)
             return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "fused encode kernel does not support this code/alignment");
     }
     return encode_staged(cs, *ds, dev, data, par, n_stripes, chunk, st);
@@ -1659,10 +1062,22 @@ extern "C" {
 int clay_abi_version(void) { return CLAY_ABI_VERSION; }
 const char *clay_build_info(void) { return "clay_amd " __DATE__ " gfx950 HIP"; }
 int clay_set_encode_path(int mode) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    int prev = g_encode_mode;
-    g_encode_mode = mode & 0xFF;
-    g_bs_pg = (mode >> 8) & 0xFF;
+    // low byte: path; next byte: variant.  Only paths that produce the reference's parity
+    // exist; unknown paths or variants are rejected (-1) and leave the setting unchanged.
+    const int path = mode & 0xFF, tile = (mode >> 8) & 0xFF;
+    if (mode < 0 || (mode >> 16) != 0) return -1;
+    bool ok = false;
+    switch (path) {
+    case kModeAuto: case kModeStaged: case kModeFused: ok = tile == 0; break;
+    case kModeBs: ok = tile == 0 || tile == 1 || tile == 4; break;     // v1 lanes of 32 B per column group
+    case kModeBs6: ok = tile == 0 || tile == 4; break;                // 256- / 128-byte tiles
+    case kModeStream: ok = tile == 0 || tile == 1 || tile == 2 || tile == 4; break;  // loader waves
+    default: ok = false;
+    }
+    if (!ok) return -1;
+    const int prev = g_encode_mode.load() | (g_encode_tile.load() << 8);
+    g_encode_tile.store(tile);
+    g_encode_mode.store(path);
     return prev;
 }
 const char *clay_last_encode_path(void) { return t_last_path.c_str(); }
@@ -1806,12 +1221,6 @@ int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, con
 // size w), one device encode of that piece, and one 2D copy of each parity piece
 // back.  Pieces round-robin over `ns` streams, so H2D of piece p+1, the encode of
 // piece p and the D2H of piece p-1 overlap (PCIe is full duplex).
-int clay_set_exec_mode(int mode) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    int prev = g_exec_mode;
-    if (mode >= 0 && mode <= 2) g_exec_mode = mode;
-    return prev;
-}
 
 int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *data_chunks,
                                uint8_t *const *parity_chunks, size_t chunk, int device, size_t piece_bytes,

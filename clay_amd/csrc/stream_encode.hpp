@@ -1,0 +1,420 @@
+// stream_encode.hpp -- the encode kernel for codes with q = 4, t = 4 (alpha = 256), e.g. the
+// BASELINE (10,4,13): loader waves stream the data through per-node LDS buffers while
+// compute waves run the bit-sliced GF(2^8) math of bitslice6.hpp.
+//
+// Data flow per workgroup (one per CU, 160 KiB LDS):
+//  * A tile is W = 256 byte positions of every (node, layer) sub-chunk row.  It is
+//    processed as 12 steps (group g = layer digit d3, data section Y = 0..2); step (g, Y)
+//    reads the real nodes of section Y at the 64 layers with d3 = g (16 KiB per node).
+//  * LDS holds one 16 KiB buffer per real data node.  Step s reads section Y's buffers;
+//    sections Y+1 and Y+2 hold steps s+1 and s+2 (landed or in flight), so 6-8 node
+//    buffers (96-128 KiB) stream while a step computes.
+//  * Dedicated loader waves (LOADERS of them) issue every LDS-DMA (16-byte
+//    global_load_lds_dwordx4, 1 KiB per instruction) and do every vmcnt wait: after the
+//    barrier of step s they refill the buffers step s-1 read with step s+2, then wait
+//    (counted) for step s+1 and join the next barrier.  Compute waves never wait on
+//    memory -- their only synchronisation is the one barrier per step -- and never
+//    issue DMA, so their issue slots go to the XOR networks.
+//  * Compute (8 waves, 512 lanes): lane = (column c, part).  The math is bitslice6.hpp's
+//    v6 kernel: PRT in the byte domain, 8x8 bit transpose, the RS generator as
+//    compile-time XOR networks into 4 x 8 plane accumulators, PFT in registers at the end
+//    of each group, transposed back and stored.
+//  * A lane's 32 positions are bytes [16p, 16p+16) and [128+16p, 128+16p+16) of the tile
+//    (p = part), so each 16-byte parity store instruction of a wave writes 8 rows x 128
+//    contiguous bytes -- whole cache lines (bench_tools/ring_probe: 8 % faster than the
+//    v6 layout's 16-byte-gapped pairs).
+//  * Tiles: every XCD owns a contiguous byte region of the sub-chunks; its workgroups
+//    take full tiles round robin (adjacent workgroups stream adjacent 256-byte runs of the
+//    same rows), and the remainder is cut into one partial tile per workgroup, always its
+//    last (bench_tools/ring_probe: XCD-blocked order streams 17 % faster than a global
+//    round robin and 25 % faster than one contiguous range per workgroup).
+//
+// Same linear map as the reference (decode_layered with erased = parity, decode.rs:167-257),
+// so the bytes are identical to the oracle's.
+#pragma once
+
+#include "bitslice6.hpp"
+
+namespace clay {
+namespace bs {
+
+// a wave-uniform pointer the compiler cannot prove uniform -> SGPRs (for the asm "s" operand)
+__device__ __forceinline__ const uint8_t *uniform_ptr(const uint8_t *p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v)), hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    return reinterpret_cast<const uint8_t *>((uint64_t(hi) << 32) | lo);
+}
+
+struct StreamTile {
+    uint32_t b0, vend;  // positions [b0, b0 + 256) of every row, valid below vend
+};
+
+// XCD x owns bytes [x * region, min((x + 1) * region, sc)); full tiles round robin over
+// the XCD's ns workgroups, the remainder one partial tile per workgroup (its last).
+struct StreamMap {
+    uint32_t x0, x1, nfull, p0, p1;
+    __device__ StreamMap(uint32_t sc, uint32_t region, uint32_t ns, uint32_t xcd, uint32_t slot) {
+        x0 = xcd * region;
+        x1 = x0 + region < sc ? x0 + region : sc;
+        nfull = p0 = p1 = 0;
+        if (x0 >= x1) return;
+        const uint32_t len = x1 - x0, round = ns * 256u;
+        nfull = len / round;
+        const uint32_t left = len - nfull * round;
+        const uint32_t wp = ((left + ns - 1) / ns + 31u) & ~31u;
+        const uint32_t q0 = x0 + nfull * round + slot * wp;
+        if (left && q0 < x1) {
+            p0 = q0;
+            p1 = q0 + wp < x1 ? q0 + wp : x1;
+        }
+    }
+    __device__ int ntile() const { return int(nfull) + (p0 < p1 ? 1 : 0); }
+    __device__ StreamTile tile(int k, uint32_t slot, uint32_t ns) const {
+        if (uint32_t(k) < nfull) {
+            const uint32_t b0 = x0 + (uint32_t(k) * ns + slot) * 256u;
+            return {b0, b0 + 256u};
+        }
+        return {p0, p1};
+    }
+};
+
+template <int KD, int LOADERS, bool COALESCED_PROBE = false>
+struct StreamEnc {
+    using K6 = Bs6Kernel<KD, 4, 8>;
+    using MP = typename K6::MP;
+    using S = typename K6::S;
+    static constexpr int Q = 4, T = 4, W = 256, CWAVES = 8;
+    static constexpr int BLOCK = 64 * (CWAVES + LOADERS);
+    static constexpr int NODE_BYTES = K6::NODE_BYTES;  // 64 layers x 256 B = 16 KiB
+    static constexpr int REGION = Q * NODE_BYTES;      // section Y's nodes: buffers 4Y .. 4Y+3
+    static constexpr int LDS_BYTES = KD * NODE_BYTES;
+    static constexpr int STEPS = 12;
+    // DMA issuers: the LOADERS dedicated waves, or (LOADERS == 0) the 8 compute waves
+    static constexpr int DMA_WAVES = LOADERS ? LOADERS : CWAVES;
+    static constexpr int BPL = 16 / DMA_WAVES;  // 1 KiB blocks of every node buffer per issuing wave
+    static_assert(LOADERS == 0 || LOADERS == 1 || LOADERS == 2 || LOADERS == 4, "loader waves");
+    static_assert(KD >= 9 && KD <= 10 && LDS_BYTES <= 160 * 1024, "one 16 KiB buffer per data node");
+    static_assert(NODE_BYTES == 16384 && K6::PB == 3, "geometry");
+
+    static constexpr int nreal(int y) {
+        int n = 0;
+        for (int x = 0; x < Q; x++) n += (y * Q + x < KD);
+        return n;
+    }
+    // instructions one loader wave issues for a step of section y
+    static constexpr int ninstr(int y) { return nreal(y) * BPL; }
+    // parity stores (16-byte instructions) a lane issues at the end of group g (full tile)
+    static constexpr int nstores(int g) { return 2 * (1 + 2 * g); }
+
+    // position (relative to the tile) of piece v = c | part << 6 | d << 9
+    __device__ static uint32_t piece_pos(uint32_t v) { return ((v >> 6) & 7u) * 16u + (v >> 9) * 128u; }
+    // the piece a loader lane fills in block blk of node-in-section x
+    __device__ static uint32_t piece_of(uint32_t vl, int blk, int x) {
+        return vl ^ MP::inv_d((uint32_t(blk) << 6) ^ MP::hbank(x));
+    }
+
+    // ---------------- loader ----------------
+    struct Loader {
+        uint32_t off[Q][BPL];  // per (node-in-section, block): lane offset in its node chunk, g = b0 = 0
+        uint32_t vl;
+        int li;
+    };
+    __device__ static void loader_init(Loader &L, uint32_t sc, int li, int lane) {
+        L.li = li;
+        L.vl = MP::inv_d(uint32_t(lane));
+#pragma unroll
+        for (int x = 0; x < Q; x++)
+#pragma unroll
+            for (int j = 0; j < BPL; j++) {
+                const uint32_t v = piece_of(L.vl, li * BPL + j, x);
+                L.off[x][j] = (v & 63u) * 4u * sc + piece_pos(v);
+                if (COALESCED_PROBE)  // probe only: 4 rows x 256 B per instruction (LDS image wrong)
+                    L.off[x][j] = uint32_t((li * BPL + j) * 4 + lane / 16) * 4u * sc + uint32_t(lane % 16) * 16u;
+            }
+    }
+    // DMA of step (section Y, group g) of tile t into section Y's node buffers
+    template <int Y>
+    __device__ static void issue(const BsArgs &a, const Loader &L, uint32_t lds0, StreamTile t, int g) {
+        const uint32_t sc = uint32_t(a.sc);
+        const bool full = t.vend >= t.b0 + uint32_t(W);
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            if constexpr (node < KD) {
+                const uint32_t dst = lds0 + uint32_t(node * NODE_BYTES) + uint32_t(L.li * BPL) * 1024u;
+                if (full) {
+                    const uint8_t *base = uniform_ptr(a.data[node] + (uint64_t(g) * sc + t.b0));
+#pragma unroll
+                    for (int j = 0; j < BPL; j++) dma16(dst + uint32_t(j) * 1024u, base, L.off[x][j]);
+                } else {
+                    // partial tile: a piece straddling vend is read from vend - 16 (patched
+                    // after landing), a piece wholly past vend from b0 (never used)
+                    const uint8_t *base = uniform_ptr(a.data[node] + uint64_t(g) * sc);
+                    uint32_t vl = L.vl;
+                    asm volatile("" : "+v"(vl));  // recomputed per call, not hoisted
+#pragma unroll
+                    for (int j = 0; j < BPL; j++) {
+                        const uint32_t v = piece_of(vl, L.li * BPL + j, x);
+                        uint32_t pos = t.b0 + piece_pos(v);
+                        if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
+                        dma16(dst + uint32_t(j) * 1024u, base, (v & 63u) * 4u * sc + pos);
+                    }
+                }
+            }
+        });
+    }
+    __device__ static void issue_any(int y, const BsArgs &a, const Loader &L, uint32_t lds0, StreamTile t, int g) {
+        if (y == 0) issue<0>(a, L, lds0, t, g);
+        else if (y == 1) issue<1>(a, L, lds0, t, g);
+        else issue<2>(a, L, lds0, t, g);
+    }
+    // A partial tile whose end is not 16-byte aligned (sc % 16 == 8): the straddling piece
+    // of every row holds 8 valid bytes; rewrite it in LDS from global memory (after the
+    // DMA of the step has landed).
+    template <int Y>
+    __device__ static void patch(const BsArgs &a, const Loader &L, uint8_t *smem, StreamTile t, int g, int lane) {
+        const uint32_t sc = uint32_t(a.sc);
+        uint32_t vl = L.vl;
+        asm volatile("" : "+v"(vl));
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr int node = Y * Q + x;
+            if constexpr (node < KD) {
+#pragma unroll
+                for (int j = 0; j < BPL; j++) {
+                    const int blk = L.li * BPL + j;
+                    const uint32_t v = piece_of(vl, blk, x);
+                    const uint32_t pos = t.b0 + piece_pos(v);
+                    if (pos < t.vend && pos + 16u > t.vend) {
+                        const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
+                        const uint2 gv = *reinterpret_cast<const uint2 *>(a.data[node] + uint64_t(layer) * sc + pos);
+                        *reinterpret_cast<uint4 *>(smem + node * NODE_BYTES + blk * 1024 + lane * 16) =
+                            make_uint4(gv.x, gv.y, 0u, 0u);
+                    }
+                }
+            }
+        });
+    }
+    __device__ static void patch_any(int y, const BsArgs &a, const Loader &L, uint8_t *smem, StreamTile t, int g,
+                                     int lane) {
+        if (y == 0) patch<0>(a, L, smem, t, g, lane);
+        else if (y == 1) patch<1>(a, L, smem, t, g, lane);
+        else patch<2>(a, L, smem, t, g, lane);
+    }
+
+    // ---------------- compute ----------------
+    // One step: the 4 nodes of section Y (own + companion reads, PRT, transpose, RS fold),
+    // each node's LDS reads issued one node ahead; the scheduling barrier after every node
+    // keeps the compiler from hoisting more reads (register pressure: 3 waves per SIMD).
+    template <int Y>
+    __device__ static void section(const uint8_t *slot, const typename K6::LaneC &L, uint32_t (&acc)[Q * 8]) {
+        uint32_t o[2][8], cv[2][8];
+        K6::template load_x<Y, 0>(slot, L, o[0], cv[0]);
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            if constexpr (x + 1 < Q) K6::template load_x<Y, x + 1>(slot, L, o[(x + 1) & 1], cv[(x + 1) & 1]);
+            uint32_t u[8];
+            K6::template prt_x<Y, x>(o[x & 1], cv[x & 1], L, u);
+            K6::template fold_x<Y, x>(u, acc);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    }
+
+    // ---------------- compute: outputs ----------------
+    // Parity C (8 planes) -> bytes -> HBM at parity node X, layer z, this lane's pieces.
+    template <int X>
+    __device__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, StreamTile t, uint32_t prel,
+                               bool ragged) {
+        transpose8(cv);
+        uint32_t off = z * uint32_t(a.sc);
+        asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
+        off += t.b0 + prel;
+        if (!ragged) {
+            st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
+            st16s(a.par[X], off + 128u, cv[4], cv[5], cv[6], cv[7]);
+        } else {
+            uint8_t *p = a.par[X] + off;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t pos = t.b0 + prel + 128u * uint32_t(h);
+                const uint32_t nv = pos >= t.vend ? 0u : (t.vend - pos >= 16u ? 16u : t.vend - pos);
+                if (nv == 16u)
+                    *reinterpret_cast<uint4 *>(p + 128 * h) = make_uint4(cv[4 * h], cv[4 * h + 1], cv[4 * h + 2], cv[4 * h + 3]);
+                else if (nv >= 8u)
+                    *reinterpret_cast<uint2 *>(p + 128 * h) = make_uint2(cv[4 * h], cv[4 * h + 1]);
+            }
+        }
+    }
+    // Group G finished: red vertex C[G][z_G] = U, and the PFT pairs with groups h < G
+    // (transforms.rs:108-125) -- the v6 schedule, see Bs6Kernel::end_group.
+    template <int G>
+    __device__ static void end_group(const BsArgs &a, const uint32_t (&acc)[Q * 8], typename K6::Hold &H, int c,
+                                     StreamTile t, uint32_t prel, bool ragged) {
+        const uint32_t zg = uint32_t(c * 4 + G);
+        uint32_t cv[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) cv[w] = acc[G * 8 + w];
+        put<G>(a, cv, zg, t, prel, ragged);
+        auto pair = [&](const uint32_t *uh_at_g, const uint32_t *ug_at_h, auto hc) BS_INL {
+            constexpr int h = decltype(hc)::value;
+            const uint32_t zh = uint32_t(c * 4 + h);
+            uint32_t c1[8], c2[8];
+            K6::pft(uh_at_g, ug_at_h, c1);  // C[h][z_G]
+            put<h>(a, c1, zg, t, prel, ragged);
+            K6::pft(ug_at_h, uh_at_g, c2);  // C[G][z_h]
+            put<G>(a, c2, zh, t, prel, ragged);
+        };
+        auto keep = [&](int ri, int p) BS_INL {
+#pragma unroll
+            for (int w = 0; w < 8; w++) H.r[ri][w] = acc[p * 8 + w];
+        };
+        if constexpr (G == 0) {
+            keep(0, 1);
+            keep(1, 2);
+            keep(2, 3);
+        } else if constexpr (G == 1) {
+            pair(acc + 0, H.r[0], std::integral_constant<int, 0>{});  // U[1][z0]
+            keep(0, 2);
+            keep(3, 3);
+        } else if constexpr (G == 2) {
+            pair(acc + 0, H.r[1], std::integral_constant<int, 0>{});  // U[2][z0]
+            pair(acc + 8, H.r[0], std::integral_constant<int, 1>{});  // U[2][z1]
+            keep(1, 3);
+        } else {
+            pair(acc + 0, H.r[2], std::integral_constant<int, 0>{});   // U[3][z0]
+            pair(acc + 8, H.r[3], std::integral_constant<int, 1>{});   // U[3][z1]
+            pair(acc + 16, H.r[1], std::integral_constant<int, 2>{});  // U[3][z2]
+        }
+    }
+};
+
+// a.tiles_per_xcd = XCD region length in bytes (multiple of 32), a.nslots = workgroups per
+// XCD; grid = 8 * nslots; LDS = KD x 16 KiB (one workgroup per CU).
+// PROBE is for bench_tools/stream_probe.hip only (the library instantiates PROBE = 0):
+// bit 1 = compute waves skip the math, 2 = loaders skip the DMA, 4 = no parity stores,
+// 8 = coalesced DMA pattern (4 rows x 256 B per instruction; with bit 1 only).
+template <int KD, int LOADERS, int PROBE = 0>
+__global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
+    using Kn = StreamEnc<KD, LOADERS, (PROBE & 8) != 0>;
+    using K6 = typename Kn::K6;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, ns = a.nslots;
+    const StreamMap tm(uint32_t(a.sc), a.tiles_per_xcd, ns, xcd, slot);
+    const int ntile = tm.ntile();
+    if (ntile == 0) return;  // uniform per workgroup
+    const int nsteps = ntile * Kn::STEPS;
+    if (LOADERS > 0 && wave >= Kn::CWAVES) {
+        // ---- loader wave ----
+        // top issue priority: a loader issues a few instructions per step and otherwise
+        // waits, but as the youngest wave on its SIMD it would lose every arbitration to the
+        // compute waves and delay the whole pipeline (measured: 1 loader 0.46 ms, 4 loaders
+        // 0.39 ms per 1 GiB stripe without this)
+        __builtin_amdgcn_s_setprio(3);
+        typename Kn::Loader L;
+        Kn::loader_init(L, uint32_t(a.sc), wave - Kn::CWAVES, lane);
+        const uint32_t lds0 = lds_addr_of(smem);
+        if constexpr (!(PROBE & 2))
+            for (int s = 0; s < 3 && s < nsteps; s++) Kn::issue_any(s % 3, a, L, lds0, tm.tile(0, slot, ns), s / 3);
+        for (int s = 0; s < nsteps; s++) {
+            const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
+            const StreamTile t = tm.tile(k, slot, ns);
+            // step s landed: everything issued after it may stay in flight
+            int after = 0;
+            if (s == 0) {
+                after = (nsteps > 1 ? Kn::ninstr(1) : 0) + (nsteps > 2 ? Kn::ninstr(2) : 0);
+            } else if (s + 1 < nsteps) {
+                after = Kn::ninstr((y + 1) % 3);
+            }
+            const bool straddle = t.vend < t.b0 + uint32_t(Kn::W) && ((t.vend - t.b0) & 15u);
+            if (PROBE & 2) {
+            } else if (straddle) {
+                wait_vm_n<0>();
+                Kn::patch_any(y, a, L, smem, t, g, lane);
+            } else {
+                wait_vm_rt(after);
+            }
+            lds_barrier();
+            // step s-1's buffers are free: refill them with step s+2
+            const int s2 = s + 2;
+            if (!(PROBE & 2) && s >= 1 && s2 < nsteps) {
+                const int k2 = s2 / Kn::STEPS, r2 = s2 % Kn::STEPS;
+                Kn::issue_any(r2 % 3, a, L, lds0, tm.tile(k2, slot, ns), r2 / 3);
+            }
+        }
+        return;
+    }
+    // ---- compute waves ----
+    const int c = int(threadIdx.x) >> 3, part = int(threadIdx.x) & 7;
+    const uint32_t prel = uint32_t(part) * 16u;
+    uint32_t acc[Kn::Q * 8];
+    typename K6::Hold H;
+    const typename K6::LaneC LC = K6::lane_consts(c, part);
+    // LOADERS == 0: every compute wave issues its share of the DMA right after each barrier
+    // and does the counted wait itself (VMEM ops after step s's DMA: the next step's DMA
+    // and the parity stores of the two steps in between)
+    typename Kn::Loader LD;
+    const uint32_t lds0 = lds_addr_of(smem);
+    if constexpr (LOADERS == 0) {
+        Kn::loader_init(LD, uint32_t(a.sc), wave, lane);
+        if constexpr (!(PROBE & 2))
+            for (int s = 0; s < 3 && s < nsteps; s++) Kn::issue_any(s % 3, a, LD, lds0, tm.tile(0, slot, ns), s / 3);
+    }
+    int st1 = 0, st2 = 0;  // counted stores issued in steps s-1 and s-2
+    for (int s = 0; s < nsteps; s++) {
+        const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
+        if constexpr (LOADERS == 0 && !(PROBE & 2)) {
+            const StreamTile t = tm.tile(k, slot, ns);
+            int after;
+            if (s == 0) after = (nsteps > 1 ? Kn::ninstr(1) : 0) + (nsteps > 2 ? Kn::ninstr(2) : 0);
+            else if (s == 1) after = (nsteps > 2 ? Kn::ninstr(2) : 0) + st1;
+            else after = st2 + (s + 1 < nsteps ? Kn::ninstr((y + 1) % 3) : 0) + st1;
+            if (t.vend < t.b0 + uint32_t(Kn::W) && ((t.vend - t.b0) & 15u)) {
+                wait_vm_n<0>();
+                Kn::patch_any(y, a, LD, smem, t, g, lane);
+            } else {
+                wait_vm_rt(after);
+            }
+        }
+        lds_barrier();
+        if constexpr (LOADERS == 0 && !(PROBE & 2)) {
+            const int s2 = s + 2;
+            if (s >= 1 && s2 < nsteps) {
+                const int k2 = s2 / Kn::STEPS, r2 = s2 % Kn::STEPS;
+                Kn::issue_any(r2 % 3, a, LD, lds0, tm.tile(k2, slot, ns), r2 / 3);
+            }
+        }
+        // opaque per-step copy of the lane constants: everything derived from them (read
+        // addresses, PRT masks) is recomputed per step instead of hoisted out of the tile
+        // loop into ~30 long-lived registers (which spilled at the 168-VGPR budget)
+        typename K6::LaneC L = LC;
+        asm volatile("" : "+v"(L.fown), "+v"(L.fcl[0]), "+v"(L.fcl[1]), "+v"(L.fcl[2]));
+        asm volatile("" : "+v"(L.cy[0]), "+v"(L.cy[1]), "+v"(L.cy[2]));
+        if constexpr ((PROBE & 1) != 0) {
+            if (s == 0)
+#pragma unroll
+                for (int w = 0; w < Kn::Q * 8; w++) acc[w] = (threadIdx.x * 0x9E3779B9u) ^ uint32_t(w) ^ L.fown;
+        } else {
+            if (y == 0) Kn::template section<0>(smem, L, acc);
+            else if (y == 1) Kn::template section<1>(smem + Kn::REGION, L, acc);
+            else Kn::template section<2>(smem + 2 * Kn::REGION, L, acc);
+        }
+        if (y == 2 && !(PROBE & 4)) {
+            const StreamTile t = tm.tile(k, slot, ns);
+            const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
+            if (g == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged);
+            else if (g == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged);
+            else if (g == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged);
+            else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged);
+            st2 = st1;
+            st1 = ragged ? 0 : Kn::nstores(g);  // a ragged tile's plain stores are not counted:
+                                                 // the waits then cover more than needed
+        } else {
+            st2 = st1;
+            st1 = 0;
+        }
+    }
+}
+
+}  // namespace bs
+}  // namespace clay

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CLAY_ABI_VERSION 1
+#define CLAY_ABI_VERSION 2
 
 /* ClayCode public fields (lib.rs:59-82) + the two private RS counts (lib.rs:79-81). */
 typedef struct clay_code {
@@ -185,23 +185,26 @@ int clay_repair_device_full_chunks(const clay_code_t *code, size_t lost_node, co
 int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int device,
                            clay_error_t *err);
 
-/* Encode path selection (process-wide; tests and benchmarks): low byte 0 = auto
- * (bit-sliced kernel if the code has a compiled instantiation and sub-chunks are
- * 8-byte aligned, else the byte-sliced fused kernel when parity is one y-section,
- * else the staged engine), 1 = force staged, 2 = require byte-sliced fused,
- * 3 = require bit-sliced v1 (register loads), 4 = v2 (4-byte LDS-DMA staging),
- * 5 = v3 (register accumulators), 6 = v4 (16-byte LDS-DMA, conflict-free LDS),
- * 7 = v5 (node-slot ring), 8 = v6 (column-per-lane, 256-byte tiles; auto's first
- * choice for (10,4,13), then v4).  Bits 8..15: tile override (v1: lanes per value;
- * v6: 4 = 128-byte tiles; a non-zero override keeps auto off v4/v6).  Returns the
- * previous low-byte mode. */
+/* Encode path selection (process-wide; tests and benchmarks).  Low byte = path:
+ *   0 auto      -- the streaming kernel for q = 4, t = 4 codes with k = 9 / 10 (the
+ *                  BASELINE (10,4,13)); else the bit-sliced v1 kernel if the code has a
+ *                  compiled instantiation; else the byte-sliced fused kernel when the
+ *                  parity is one y-section; else the staged plan executor.  Batches of
+ *                  >= 4 stripes of <= 4 MiB of data run as one staged launch per level.
+ *                  Bit-sliced kernels need sub-chunks that are multiples of 8 bytes
+ *                  and 8-byte aligned chunk pointers.
+ *   1 staged    -- the plan executor (k_gexec), any code
+ *   2 fused     -- byte-sliced fused kernel (q == m <= 4)
+ *   3 bitsliced -- bit-sliced v1 (register loads); variant = lanes per column group
+ *                  for (10,4,13): 0 (2), 1, 4
+ *   4 bitsliced6-- v6 (column-per-lane, 2-slot LDS ring), (10,4,13); variant 0 = 256-B
+ *                  tiles, 4 = 128-B tiles
+ *   5 stream    -- the streaming kernel (stream_encode.hpp); variant = loader waves
+ *                  0 (= 2), 1, 2, 4
+ * Bits 8..15 = variant.  Every accepted (path, variant) produces the reference's
+ * parity bytes; any other value returns -1 and leaves the setting unchanged.
+ * Returns the previous setting (path | variant << 8). */
 int clay_set_encode_path(int mode);
-
-/* Plan executor for decode / repair / staged encode (process-wide; tests and
- * benchmarks): 0 = one op per block (k_exec), 1 = source-sharing op groups
- * (k_gexec, default), 2 = fused tile executor with the U plane in LDS (k_fexec;
- * plans that do not fit LDS run grouped).  Returns the previous mode. */
-int clay_set_exec_mode(int mode);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
 const char *clay_last_encode_path(void);

@@ -34,12 +34,33 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared_functions())
 
 
+SHIPPING_KERNELS = {"k_stream_encode", "k_bs_encode", "k_bs6_encode", "k_fused_encode", "k_gexec"}
+
+
+def kernel_names(blob: bytes):
+    """Kernel names in the embedded gfx950 code object (Itanium-mangled `<len><name>`)."""
+    names = set()
+    for m in re.finditer(rb"(\d+)(k_[a-z0-9_]+)", blob):
+        n = int(m.group(1)[-2:]) if len(m.group(1)) > 1 and int(m.group(1)[-2:]) <= len(m.group(2)) else int(m.group(1)[-1:])
+        if n == len(m.group(2)):
+            names.add(m.group(2).decode())
+    return names
+
+
 def test_library_is_gfx950_hip_binary():
     path = _lib.LIB_PATH
     blob = open(path, "rb").read()
     assert b"gfx950" in blob, "no gfx950 code object in libclay_amd.so"
-    assert b"k_fused_encode" in blob and b"k_exec" in blob
-    assert _lib.lib().clay_abi_version() == 1
+    assert _lib.lib().clay_abi_version() == 2
+
+
+def test_library_ships_only_parity_producing_kernels():
+    """Measurement probes and superseded encode variants live in bench_tools/ (their own
+    binaries), never in the product library: every kernel in libclay_amd.so is one that
+    produces the reference's bytes (tests/test_gpu_parity.py checks each against the oracle)."""
+    names = kernel_names(open(_lib.LIB_PATH, "rb").read())
+    assert SHIPPING_KERNELS <= names, SHIPPING_KERNELS - names
+    assert names <= SHIPPING_KERNELS, names - SHIPPING_KERNELS
 
 
 def test_error_struct_layout_matches_oracle(oracle_mod):

@@ -1,0 +1,47 @@
+"""bench.py's own 1 -> N launcher, exercised on CPU (gloo, world_size 2).
+
+`python bench.py --gpus N` without an external torchrun spawns N rank processes
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* = 127.0.0.1) before touching HIP; this is
+the code the driver's `--gpus 8` run hits.  `--cpu-dry` swaps only the device encode
+for the oracle and RCCL for gloo, so the launcher, the barrier-bracketed timing, the
+per-rank gather and the JSON line are the production ones."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True,
+                       text=True, timeout=timeout, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_launcher_cpu_dry(oracle_mod, world):
+    stripe = 10 * 256 * 2 * 64  # sc = 128
+    d = _run(["--gpus", str(world), "--cpu-dry", "--stripe-bytes", str(stripe), "--steps", "3",
+              "--warmup", "1", "--cpu-seconds", "0"])
+    assert d["n_gpus"] == world
+    assert d["cpu_dry"] is True
+    assert len(d["per_rank"]["wall_ms_per_step"]) == world
+    assert all(d["per_rank"]["verified"])
+    assert d["scaling"] == "weak" and d["steps"] == 3
+    assert d["config"]["parallelism"] == f"stripe-per-gpu x{world}"
+    # value = all ranks' bytes / the slowest rank's time
+    padded = d["config"]["padded_stripe_bytes"]
+    slowest = max(d["per_rank"]["wall_ms_per_step"]) * 1e-3 * d["steps"]
+    assert d["value"] == pytest.approx(world * d["steps"] * padded / slowest / 2**30, rel=0.02)
+    for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "vs_baseline", "dtype",
+                "data", "config", "roofline"):
+        assert key in d

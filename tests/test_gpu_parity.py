@@ -32,14 +32,6 @@ def _auto_path():
     set_encode_path("auto")
 
 
-@pytest.fixture(params=["grouped", "fused", "ops"])
-def exec_mode(request):
-    """Run a test under each plan executor (k_gexec default, k_fexec, k_exec)."""
-    prev = clay_amd.set_exec_mode(request.param)
-    yield request.param
-    clay_amd.set_exec_mode(prev)
-
-
 @pytest.mark.parametrize("cfg", CONFIGS)
 @pytest.mark.parametrize("size_kind", ["empty", "tiny", "ragged", "aligned16", "sc2", "big"])
 def test_encode_matches_oracle(oracle_mod, cfg, size_kind):
@@ -76,49 +68,59 @@ def test_bitsliced_encode_matches_oracle(oracle_mod, cfg, tile, scale):
     assert np.array_equal(got, ref), (cfg, tile, scale)
 
 
-@pytest.mark.parametrize("variant", ["bitsliced2", "bitsliced3"])
-@pytest.mark.parametrize("cfg", [(10, 4, 13), (8, 4, 11)])
-@pytest.mark.parametrize("scale", [1, 2, 3, 37, 200, 1000])
-def test_bitsliced23_encode_matches_oracle(oracle_mod, cfg, scale, variant):
-    """v3 is instantiated for (10,4,13) only.
-    LDS-DMA staged bit-sliced kernel: single/multiple tiles, ragged last tile,
-    and more tiles than workgroups (persistent loop + cross-tile prefetch)."""
-    if variant == "bitsliced3" and cfg != (10, 4, 13):
-        pytest.skip("v3 only instantiated for (10,4,13)")
+STREAM_SC = [16, 24, 64, 72, 104, 128, 256, 1064, 6440, 8 * 256 * 32, 8 * 256 * 32 + 8, 64 * 300 + 40,
+             64 * 2000 + 8, 8 * 256 * 32 * 3 + 4096 + 24]
+
+
+@pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
+@pytest.mark.parametrize("loaders", [0, 1, 2])
+@pytest.mark.parametrize("sc", STREAM_SC)
+def test_stream_encode_matches_oracle(oracle_mod, cfg, loaders, sc):
+    """Streaming kernel (q = 4, t = 4): tiny sub-chunks (one partial tile), exact XCD
+    rounds, sc % 16 == 8 (straddling piece patched in LDS), partial tiles of every
+    width and more tiles than workgroups; 1 / 2 / 4 loader waves."""
     k, m, d = cfg
-    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
-    n = k * c.sub_chunk_no * 8 * scale * 4 - 11
-    data = rand_bytes(scale * 13, n)
-    ref = o.encode_array(data)
-    set_encode_path(variant)
-    got = c.encode_array(data)
-    assert last_encode_path().startswith(variant), last_encode_path()
-    assert np.array_equal(got, ref), (cfg, scale)
-
-
-@pytest.mark.parametrize("variant", ["bitsliced4", "bitsliced5", "bitsliced6", "bitsliced6:4", "bitsliced6:20", "bitsliced6:24", "bitsliced6:40",
-                                     "bitsliced7", "bitsliced7:1", "bitsliced8"])
-@pytest.mark.parametrize("sc", [64, 72, 104, 128, 1064, 6440, 64 * 300 + 40, 64 * 2000 + 8])
-def test_bitsliced456_encode_matches_oracle(oracle_mod, sc, variant):
-    """v4 (16-byte LDS-DMA, swizzled stage / accumulator) and v5 (register
-    accumulators, node-slot ring), (10,4,13) only.  sc % 16 == 8
-    sizes put an 8-valid-byte piece in the last tile (DMA'd clamped, patched in LDS);
-    64 * 2000 + 8 has more tiles than workgroups (cross-tile prefetch)."""
-    k, m, d = 10, 4, 13
+    if loaders and cfg != (10, 4, 13):
+        pytest.skip("loader variants are instantiated for (10,4,13)")
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     n = k * c.sub_chunk_no * sc - 7
-    data = rand_bytes(sc, n)
+    data = rand_bytes(sc + loaders, n)
     ref = o.encode_array(data)
     assert ref.shape[1] == c.sub_chunk_no * sc
-    name, _, tile = variant.partition(":")
-    set_encode_path(name, int(tile or 0))
+    set_encode_path("stream", loaders)
     got = c.encode_array(data)
-    assert last_encode_path().startswith(name), last_encode_path()
+    assert last_encode_path().startswith("stream"), last_encode_path()
+    assert np.array_equal(got, ref), (cfg, sc, loaders)
+
+
+@pytest.mark.parametrize("tile", [0, 4])
+@pytest.mark.parametrize("sc", [64, 72, 1064, 64 * 300 + 40, 64 * 2000 + 8])
+def test_bitsliced6_encode_matches_oracle(oracle_mod, sc, tile):
+    """v6 (10,4,13): ragged last tile, sc % 16 == 8, more tiles than workgroups."""
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    n = 10 * c.sub_chunk_no * sc - 7
+    data = rand_bytes(sc, n)
+    ref = o.encode_array(data)
+    set_encode_path("bitsliced6", tile)
+    got = c.encode_array(data)
+    assert last_encode_path().startswith("bitsliced6"), last_encode_path()
     assert np.array_equal(got, ref), sc
 
 
+def test_encode_path_rejects_unknown_variants():
+    """Only paths that produce the reference's parity are selectable."""
+    with pytest.raises(ValueError):
+        set_encode_path("bitsliced6", 40)
+    with pytest.raises(ValueError):
+        set_encode_path("stream", 3)
+    with pytest.raises(ValueError):
+        set_encode_path("probe")
+    assert clay_amd._lib.lib().clay_set_encode_path(9 | 2 << 8) == -1
+    assert clay_amd._lib.lib().clay_set_encode_path(12) == -1
+
+
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_encode_fused_equals_staged(oracle_mod, cfg, exec_mode):
+def test_encode_fused_equals_staged(oracle_mod, cfg):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     data = rand_bytes(7, k * c.sub_chunk_no * 2 * 16 - 5)  # sc = 32: fused-eligible
@@ -136,7 +138,7 @@ def test_encode_fused_equals_staged(oracle_mod, cfg, exec_mode):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_decode_random_inputs_match_oracle(oracle_mod, cfg, exec_mode):
+def test_decode_random_inputs_match_oracle(oracle_mod, cfg):
     """Non-codeword inputs: only the reference's exact RS row choice reproduces these bytes."""
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
@@ -162,7 +164,7 @@ def test_decode_roundtrip_max_erasures(oracle_mod, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_repair_every_node_matches_oracle(oracle_mod, cfg, exec_mode):
+def test_repair_every_node_matches_oracle(oracle_mod, cfg):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     data = rand_bytes(5, k * c.sub_chunk_no * 2 * 3)
@@ -283,10 +285,9 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
     dev = torch.from_numpy(ref[:10].copy()).cuda()
     # every encode kernel at the BASELINE size (sc = 419,432: ragged last tile, 8-byte
     # aligned sub-chunks), auto first
-    for path, tile, prefix in [("auto", 0, "bitsliced6-k10m4-w256"), ("bitsliced6", 4, "bitsliced6-k10m4-w128"),
-                               ("bitsliced7", 0, "bitsliced7"), ("bitsliced7", 1, "bitsliced7-k10m4-w256-nt"),
-                               ("bitsliced4", 0, "bitsliced4"), ("bitsliced2", 0, "bitsliced2"),
-                               ("fused", 0, "fused")]:
+    for path, tile, prefix in [("auto", 0, "stream-k10m4-w256-l4"), ("stream", 1, "stream-k10m4-w256-l1"),
+                               ("stream", 2, "stream-k10m4-w256-l2"), ("bitsliced6", 0, "bitsliced6-k10m4-w256"),
+                               ("bitsliced", 0, "bitsliced-k10m4"), ("fused", 0, "fused")]:
         par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
         set_encode_path(path, tile)
         c.encode_device([dev[i] for i in range(10)], [par[i] for i in range(4)], chunk)
@@ -336,7 +337,7 @@ def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda):
 
 @pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13)])
 @pytest.mark.parametrize("sc", [16 * 257 + 2, 16 * 1000 + 9, 16 * 3001])
-def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc, exec_mode):
+def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc):
     """Sub-chunks spanning several executor tiles whose regions start at 2-byte / odd
     offsets (the (9,3,11) 256 MiB chunk has sc = 3,314,018): random (non-codeword)
     inputs, decode and repair byte-identical to the oracle."""
@@ -380,7 +381,7 @@ def test_encode_host_pipelined_matches_oracle(oracle_mod, torch_cuda, cfg, sc, p
 
 
 @pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13), (6, 3, 8)])
-def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg, exec_mode):
+def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg):
     """Repair straight from whole helper chunks in HBM (no gather): same bytes as the
     oracle's repair on the gathered beta sub-chunks, for codewords and random chunks."""
     torch = torch_cuda
