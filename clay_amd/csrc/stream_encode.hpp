@@ -15,14 +15,18 @@
 //    (counted) for step s+1 and join the next barrier.  Compute waves never wait on
 //    memory -- their only synchronisation is the one barrier per step -- and never
 //    issue DMA, so their issue slots go to the XOR networks.
+//  * Every DMA instruction reads 4 whole 256-byte row runs (4 layers of one node), so the
+//    reads are as coalesced as a plain streaming copy; the LDS image is XOR-swizzled
+//    through the choice of piece per lane (see sw() below) so the compute reads stay
+//    bank-conflict free (bench_tools/stream_probe: coalesced DMA 0.345 vs 0.375 ms
+//    memory-only for the scattered piece map of the v6 image).
 //  * Compute (8 waves, 512 lanes): lane = (column c, part).  The math is bitslice6.hpp's
 //    v6 kernel: PRT in the byte domain, 8x8 bit transpose, the RS generator as
 //    compile-time XOR networks into 4 x 8 plane accumulators, PFT in registers at the end
 //    of each group, transposed back and stored.
 //  * A lane's 32 positions are bytes [16p, 16p+16) and [128+16p, 128+16p+16) of the tile
-//    (p = part), so each 16-byte parity store instruction of a wave writes 8 rows x 128
-//    contiguous bytes -- whole cache lines (bench_tools/ring_probe: 8 % faster than the
-//    v6 layout's 16-byte-gapped pairs).
+//    (p = part); at the parity stores neighbouring columns swap halves (DPP), so each
+//    16-byte store instruction of a wave writes 4 whole 256-byte row runs.
 //  * Tiles: every XCD owns a contiguous byte region of the sub-chunks; its workgroups
 //    take full tiles round robin (adjacent workgroups stream adjacent 256-byte runs of the
 //    same rows), and the remainder is cut into one partial tile per workgroup, always its
@@ -78,15 +82,14 @@ struct StreamMap {
     }
 };
 
-template <int KD, int LOADERS, bool COALESCED_PROBE = false>
+template <int KD, int LOADERS>
 struct StreamEnc {
     using K6 = Bs6Kernel<KD, 4, 8>;
-    using MP = typename K6::MP;
     using S = typename K6::S;
     static constexpr int Q = 4, T = 4, W = 256, CWAVES = 8;
     static constexpr int BLOCK = 64 * (CWAVES + LOADERS);
-    static constexpr int NODE_BYTES = K6::NODE_BYTES;  // 64 layers x 256 B = 16 KiB
-    static constexpr int REGION = Q * NODE_BYTES;      // section Y's nodes: buffers 4Y .. 4Y+3
+    static constexpr int NODE_BYTES = 64 * W;      // 64 layers (columns c) x 256 B = 16 KiB
+    static constexpr int REGION = Q * NODE_BYTES;  // section Y's nodes: buffers 4Y .. 4Y+3
     static constexpr int LDS_BYTES = KD * NODE_BYTES;
     static constexpr int STEPS = 12;
     // DMA issuers: the LOADERS dedicated waves, or (LOADERS == 0) the 8 compute waves
@@ -94,7 +97,6 @@ struct StreamEnc {
     static constexpr int BPL = 16 / DMA_WAVES;  // 1 KiB blocks of every node buffer per issuing wave
     static_assert(LOADERS == 0 || LOADERS == 1 || LOADERS == 2 || LOADERS == 4, "loader waves");
     static_assert(KD >= 9 && KD <= 10 && LDS_BYTES <= 160 * 1024, "one 16 KiB buffer per data node");
-    static_assert(NODE_BYTES == 16384 && K6::PB == 3, "geometry");
 
     static constexpr int nreal(int y) {
         int n = 0;
@@ -105,32 +107,35 @@ struct StreamEnc {
     static constexpr int ninstr(int y) { return nreal(y) * BPL; }
     // parity stores (16-byte instructions) a lane issues at the end of group g (full tile)
     static constexpr int nstores(int g) { return 2 * (1 + 2 * g); }
+    static constexpr int dshift(int y) { return 2 * (T - 2 - y); }  // digit y of the column c
 
-    // position (relative to the tile) of piece v = c | part << 6 | d << 9
-    __device__ static uint32_t piece_pos(uint32_t v) { return ((v >> 6) & 7u) * 16u + (v >> 9) * 128u; }
-    // the piece a loader lane fills in block blk of node-in-section x
-    __device__ static uint32_t piece_of(uint32_t vl, int blk, int x) {
-        return vl ^ MP::inv_d((uint32_t(blk) << 6) ^ MP::hbank(x));
-    }
+    // ---- node-buffer image ----
+    // Row r (= column c, layer 4c + g) occupies bytes [256 r, 256 r + 256); its 16-byte
+    // piece k sits at 16-byte slot k ^ sw(r), sw(r) = 8 * bit 1 of r.  1 KiB block j holds
+    // rows 4j .. 4j+3, so ONE LDS-DMA instruction fills a block from 4 whole 256-byte row
+    // runs in HBM (coalesced); the swizzle only permutes which lane fetches which piece.
+    // Reads (lane = column c, part p; pieces p and 8 + p of a row): within every 16-lane
+    // group of ds_read_b128 the columns c, c+3 and c+1, c+2 share parts, and sw separates
+    // exactly those pairs, so own and companion reads are bank-conflict free (companions of
+    // sections 0/1 keep c mod 4; section 2's companion row is shared = broadcast).
+    __host__ __device__ static constexpr uint32_t sw(uint32_t r) { return ((r >> 1) & 1u) * 8u; }
 
     // ---------------- loader ----------------
     struct Loader {
-        uint32_t off[Q][BPL];  // per (node-in-section, block): lane offset in its node chunk, g = b0 = 0
-        uint32_t vl;
+        uint32_t off[BPL];  // per block: lane offset in its node chunk for g = 0, b0 = 0
+        uint32_t k16;       // 16 x the piece this lane fetches in every block
+        uint32_t rl;        // row-in-block of this lane
         int li;
     };
     __device__ static void loader_init(Loader &L, uint32_t sc, int li, int lane) {
         L.li = li;
-        L.vl = MP::inv_d(uint32_t(lane));
+        L.rl = uint32_t(lane) >> 4;
+        L.k16 = ((uint32_t(lane) & 15u) ^ sw(L.rl)) * 16u;
 #pragma unroll
-        for (int x = 0; x < Q; x++)
-#pragma unroll
-            for (int j = 0; j < BPL; j++) {
-                const uint32_t v = piece_of(L.vl, li * BPL + j, x);
-                L.off[x][j] = (v & 63u) * 4u * sc + piece_pos(v);
-                if (COALESCED_PROBE)  // probe only: 4 rows x 256 B per instruction (LDS image wrong)
-                    L.off[x][j] = uint32_t((li * BPL + j) * 4 + lane / 16) * 4u * sc + uint32_t(lane % 16) * 16u;
-            }
+        for (int j = 0; j < BPL; j++) {
+            const uint32_t r = uint32_t(li * BPL + j) * 4u + L.rl;
+            L.off[j] = r * 4u * sc + L.k16;
+        }
     }
     // DMA of step (section Y, group g) of tile t into section Y's node buffers
     template <int Y>
@@ -145,20 +150,15 @@ struct StreamEnc {
                 if (full) {
                     const uint8_t *base = uniform_ptr(a.data[node] + (uint64_t(g) * sc + t.b0));
 #pragma unroll
-                    for (int j = 0; j < BPL; j++) dma16(dst + uint32_t(j) * 1024u, base, L.off[x][j]);
+                    for (int j = 0; j < BPL; j++) dma16(dst + uint32_t(j) * 1024u, base, L.off[j]);
                 } else {
                     // partial tile: a piece straddling vend is read from vend - 16 (patched
                     // after landing), a piece wholly past vend from b0 (never used)
                     const uint8_t *base = uniform_ptr(a.data[node] + uint64_t(g) * sc);
-                    uint32_t vl = L.vl;
-                    asm volatile("" : "+v"(vl));  // recomputed per call, not hoisted
+                    uint32_t pos = t.b0 + L.k16;
+                    if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
 #pragma unroll
-                    for (int j = 0; j < BPL; j++) {
-                        const uint32_t v = piece_of(vl, L.li * BPL + j, x);
-                        uint32_t pos = t.b0 + piece_pos(v);
-                        if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
-                        dma16(dst + uint32_t(j) * 1024u, base, (v & 63u) * 4u * sc + pos);
-                    }
+                    for (int j = 0; j < BPL; j++) dma16(dst + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
                 }
             }
         });
@@ -174,8 +174,8 @@ struct StreamEnc {
     template <int Y>
     __device__ static void patch(const BsArgs &a, const Loader &L, uint8_t *smem, StreamTile t, int g, int lane) {
         const uint32_t sc = uint32_t(a.sc);
-        uint32_t vl = L.vl;
-        asm volatile("" : "+v"(vl));
+        const uint32_t pos = t.b0 + L.k16;
+        if (!(pos < t.vend && pos + 16u > t.vend)) return;
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
             constexpr int node = Y * Q + x;
@@ -183,14 +183,10 @@ struct StreamEnc {
 #pragma unroll
                 for (int j = 0; j < BPL; j++) {
                     const int blk = L.li * BPL + j;
-                    const uint32_t v = piece_of(vl, blk, x);
-                    const uint32_t pos = t.b0 + piece_pos(v);
-                    if (pos < t.vend && pos + 16u > t.vend) {
-                        const uint32_t layer = (v & 63u) * 4u + uint32_t(g);
-                        const uint2 gv = *reinterpret_cast<const uint2 *>(a.data[node] + uint64_t(layer) * sc + pos);
-                        *reinterpret_cast<uint4 *>(smem + node * NODE_BYTES + blk * 1024 + lane * 16) =
-                            make_uint4(gv.x, gv.y, 0u, 0u);
-                    }
+                    const uint32_t layer = (uint32_t(blk) * 4u + L.rl) * 4u + uint32_t(g);
+                    const uint2 gv = *reinterpret_cast<const uint2 *>(a.data[node] + uint64_t(layer) * sc + pos);
+                    *reinterpret_cast<uint4 *>(smem + node * NODE_BYTES + blk * 1024 + lane * 16) =
+                        make_uint4(gv.x, gv.y, 0u, 0u);
                 }
             }
         });
@@ -203,37 +199,113 @@ struct StreamEnc {
     }
 
     // ---------------- compute ----------------
+    // Per-lane LDS offsets (loop invariant).  Own value of node x: x * 16 KiB + own[h] for
+    // piece h * 8 + p.  Companion in section Y (node cy[Y] of the section, column c with
+    // digit Y := x): cb[Y][h] + x * 4^(2-Y) * 256, plus for Y = 2 the swizzle of row x.
+    struct LaneS {
+        uint32_t own[2], cb[3][2];
+        int cy[3];
+    };
+    __device__ static LaneS lane_consts(int c, int part) {
+        LaneS L;
+        const uint32_t pk = (uint32_t(part) ^ sw(uint32_t(c))) * 16u;
+        L.own[0] = uint32_t(c) * 256u + pk;
+        L.own[1] = L.own[0] ^ 128u;
+#pragma unroll
+        for (int y = 0; y < 3; y++) {
+            const int sh = dshift(y);
+            L.cy[y] = (c >> sh) & 3;
+            const uint32_t row0 = uint32_t(c & ~(3 << sh)) * 256u + uint32_t(L.cy[y]) * uint32_t(NODE_BYTES);
+            if (y < 2) {
+                L.cb[y][0] = row0 + pk;
+                L.cb[y][1] = L.cb[y][0] ^ 128u;
+            } else {
+                L.cb[y][0] = L.cb[y][1] = row0 + uint32_t(part) * 16u;
+            }
+        }
+        return L;
+    }
+    __device__ static void read32(const uint8_t *p0, const uint8_t *p1, uint32_t (&d)[8]) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(p0), v1 = *reinterpret_cast<const uint4 *>(p1);
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+    // own value and companion of node x of section Y (zero for shortened nodes)
+    template <int Y, int X>
+    __device__ static void load_x(const uint8_t *slot, const LaneS &L, uint32_t (&o)[8], uint32_t (&cv)[8]) {
+        if constexpr (Y * Q + X < KD) {
+            read32(slot + X * NODE_BYTES + L.own[0], slot + X * NODE_BYTES + L.own[1], o);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; w++) o[w] = 0;
+        }
+        if ((Y * Q + L.cy[Y]) < KD) {
+            constexpr uint32_t step = uint32_t(256) << dshift(Y);
+            if constexpr (Y < 2) {
+                read32(slot + L.cb[Y][0] + X * step, slot + L.cb[Y][1] + X * step, cv);
+            } else {
+                constexpr uint32_t s0 = sw(uint32_t(X)) * 16u;
+                read32(slot + L.cb[Y][0] + (X * step + s0), slot + L.cb[Y][0] + (X * step + (s0 ^ 128u)), cv);
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; w++) cv[w] = 0;
+        }
+    }
+    // PRT of node x in the byte domain: U = O + gamma * C* (C* masked off for the red
+    // vertex and for shortened companions), transforms.rs:42-55
+    template <int Y, int X>
+    __device__ static void prt_x(const uint32_t (&o)[8], const uint32_t (&cv)[8], const LaneS &L, uint32_t (&u)[8]) {
+        const int cy = L.cy[Y];
+        const bool creal = (Y * Q + cy) < KD;
+        const uint32_t keep = (creal && X != cy) ? 0xffffffffu : 0u;
+        const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+#pragma unroll
+        for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+    }
     // One step: the 4 nodes of section Y (own + companion reads, PRT, transpose, RS fold),
     // each node's LDS reads issued one node ahead; the scheduling barrier after every node
     // keeps the compiler from hoisting more reads (register pressure: 3 waves per SIMD).
     template <int Y>
-    __device__ static void section(const uint8_t *slot, const typename K6::LaneC &L, uint32_t (&acc)[Q * 8]) {
+    __device__ static void section(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
         uint32_t o[2][8], cv[2][8];
-        K6::template load_x<Y, 0>(slot, L, o[0], cv[0]);
+        load_x<Y, 0>(slot, L, o[0], cv[0]);
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
-            if constexpr (x + 1 < Q) K6::template load_x<Y, x + 1>(slot, L, o[(x + 1) & 1], cv[(x + 1) & 1]);
+            if constexpr (x + 1 < Q) load_x<Y, x + 1>(slot, L, o[(x + 1) & 1], cv[(x + 1) & 1]);
             uint32_t u[8];
-            K6::template prt_x<Y, x>(o[x & 1], cv[x & 1], L, u);
+            prt_x<Y, x>(o[x & 1], cv[x & 1], L, u);
             K6::template fold_x<Y, x>(u, acc);
             __builtin_amdgcn_sched_barrier(0);
         });
     }
 
     // ---------------- compute: outputs ----------------
-    // Parity C (8 planes) -> bytes -> HBM at parity node X, layer z, this lane's pieces.
+    // Parity C (8 planes) -> bytes -> HBM at parity node X, layer z = 4c + G.  A lane holds
+    // pieces p and 8 + p of its row; lanes c and c ^ 1 (lane ^ 8, same row of 16 lanes) swap
+    // halves by DPP so that each 16-byte store instruction of a wave writes 4 whole
+    // 256-byte row runs (even columns, then odd columns) instead of 8 rows x 128 B.
     template <int X>
     __device__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, StreamTile t, uint32_t prel,
                                bool ragged) {
         transpose8(cv);
-        uint32_t off = z * uint32_t(a.sc);
-        asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
-        off += t.b0 + prel;
         if (!ragged) {
-            st16s(a.par[X], off, cv[0], cv[1], cv[2], cv[3]);
-            st16s(a.par[X], off + 128u, cv[4], cv[5], cv[6], cv[7]);
+            const bool odd = (threadIdx.x >> 3) & 1u;
+            uint32_t r[4], lo[4], hi[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t send = odd ? cv[i] : cv[4 + i];
+                r[i] = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, false));  // row_ror:8
+                lo[i] = odd ? r[i] : cv[i];      // row of the even column, piece (odd ? 8 : 0) + p
+                hi[i] = odd ? cv[4 + i] : r[i];  // row of the odd column
+            }
+            uint32_t off = (z - (odd ? 4u : 0u)) * uint32_t(a.sc);
+            asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
+            off += t.b0 + prel + (odd ? 128u : 0u);
+            st16s(a.par[X], off, lo[0], lo[1], lo[2], lo[3]);
+            st16s(a.par[X], off + 4u * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
         } else {
-            uint8_t *p = a.par[X] + off;
+            uint8_t *p = a.par[X] + uint64_t(z) * a.sc + t.b0 + prel;
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const uint32_t pos = t.b0 + prel + 128u * uint32_t(h);
@@ -292,10 +364,10 @@ struct StreamEnc {
 // XCD; grid = 8 * nslots; LDS = KD x 16 KiB (one workgroup per CU).
 // PROBE is for bench_tools/stream_probe.hip only (the library instantiates PROBE = 0):
 // bit 1 = compute waves skip the math, 2 = loaders skip the DMA, 4 = no parity stores,
-// 8 = coalesced DMA pattern (4 rows x 256 B per instruction; with bit 1 only).
+// 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1.
 template <int KD, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
-    using Kn = StreamEnc<KD, LOADERS, (PROBE & 8) != 0>;
+    using Kn = StreamEnc<KD, LOADERS>;
     using K6 = typename Kn::K6;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -310,7 +382,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         // waits, but as the youngest wave on its SIMD it would lose every arbitration to the
         // compute waves and delay the whole pipeline (measured: 1 loader 0.46 ms, 4 loaders
         // 0.39 ms per 1 GiB stripe without this)
-        __builtin_amdgcn_s_setprio(3);
+        if constexpr (!(PROBE & 8)) __builtin_amdgcn_s_setprio(3);
         typename Kn::Loader L;
         Kn::loader_init(L, uint32_t(a.sc), wave - Kn::CWAVES, lane);
         const uint32_t lds0 = lds_addr_of(smem);
@@ -345,11 +417,14 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         return;
     }
     // ---- compute waves ----
+    if constexpr ((PROBE & 16) != 0) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     const int c = int(threadIdx.x) >> 3, part = int(threadIdx.x) & 7;
     const uint32_t prel = uint32_t(part) * 16u;
     uint32_t acc[Kn::Q * 8];
     typename K6::Hold H;
-    const typename K6::LaneC LC = K6::lane_consts(c, part);
+    const typename Kn::LaneS LC = Kn::lane_consts(c, part);
     // LOADERS == 0: every compute wave issues its share of the DMA right after each barrier
     // and does the counted wait itself (VMEM ops after step s's DMA: the next step's DMA
     // and the parity stores of the two steps in between)
@@ -387,13 +462,14 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         // opaque per-step copy of the lane constants: everything derived from them (read
         // addresses, PRT masks) is recomputed per step instead of hoisted out of the tile
         // loop into ~30 long-lived registers (which spilled at the 168-VGPR budget)
-        typename K6::LaneC L = LC;
-        asm volatile("" : "+v"(L.fown), "+v"(L.fcl[0]), "+v"(L.fcl[1]), "+v"(L.fcl[2]));
+        typename Kn::LaneS L = LC;
+        asm volatile("" : "+v"(L.own[0]), "+v"(L.own[1]), "+v"(L.cb[0][0]), "+v"(L.cb[0][1]));
+        asm volatile("" : "+v"(L.cb[1][0]), "+v"(L.cb[1][1]), "+v"(L.cb[2][0]));
         asm volatile("" : "+v"(L.cy[0]), "+v"(L.cy[1]), "+v"(L.cy[2]));
         if constexpr ((PROBE & 1) != 0) {
             if (s == 0)
 #pragma unroll
-                for (int w = 0; w < Kn::Q * 8; w++) acc[w] = (threadIdx.x * 0x9E3779B9u) ^ uint32_t(w) ^ L.fown;
+                for (int w = 0; w < Kn::Q * 8; w++) acc[w] = (threadIdx.x * 0x9E3779B9u) ^ uint32_t(w) ^ L.own[0];
         } else {
             if (y == 0) Kn::template section<0>(smem, L, acc);
             else if (y == 1) Kn::template section<1>(smem + Kn::REGION, L, acc);

@@ -22,7 +22,8 @@ tail -2 gpurun_out/${TAG}_bench.log
 echo "[$(date +%T)] rocprofv3 kernel trace"
 export TMPDIR=/tmp
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o enc --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-verify --no-host-path --cpu-seconds 0 ) > gpurun_out/${TAG}_rocprof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/${TAG}_rocprof.log; exit 1; }
-find gpurun_out/${TAG}_prof -name "*stats*" | head
+find gpurun_out/${TAG}_prof -type f ! -name "*stats*" -delete
+find gpurun_out/${TAG}_prof -name "*stats*"
 if [ -n "$PMC" ]; then
 echo "[$(date +%T)] PMC passes"
 bash scripts/prof_pmc.sh ${TAG}_pmc auto 0 || { echo "pmc failed"; exit 1; }
