@@ -108,6 +108,19 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
+def release_workspace(device: int = 0) -> None:
+    """Free the device's idle pooled buffers and batch pointer tables (clay.h)."""
+    err = ClayErrorStruct()
+    rc = _lib.lib().clay_release_workspace(int(device), C.byref(err))
+    if rc:
+        _raise(rc, err)
+
+
+def workspace_bytes(device: int = 0) -> int:
+    """Device memory held by the device's buffer pool."""
+    return int(_lib.lib().clay_workspace_bytes(int(device)))
+
+
 def last_encode_path() -> str:
     return _lib.lib().clay_last_encode_path().decode()
 
@@ -241,6 +254,13 @@ class ClayCode:
         rc = _lib.lib().clay_encode_device_batch(C.byref(self._c), dp, pp, int(n_stripes),
                                                  int(chunk_size), int(device),
                                                  C.c_void_p(int(stream)), C.byref(err))
+        if rc:
+            _raise(rc, err)
+
+    def reserve_workspace(self, chunk_size: int, device: int = 0):
+        """Pre-allocate a pooled workspace and upload the encode plan (clay.h)."""
+        err = ClayErrorStruct()
+        rc = _lib.lib().clay_reserve_workspace(C.byref(self._c), int(chunk_size), int(device), C.byref(err))
         if rc:
             _raise(rc, err)
 

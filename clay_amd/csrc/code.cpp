@@ -148,6 +148,12 @@ Error validate_decode(const clay_code_t &c, const AvailView &av, const size_t *e
             return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0,
                               "Invalid parameters: Node %zu is neither erased nor provided in available chunks",
                               node);
+    // decode_layered builds ReedSolomon::new(original_count, recovery_count) before any
+    // layer work, even with no data node erased (decode.rs:175-180): galois_8 allows at
+    // most 256 shards
+    if (c.original_count + c.recovery_count > 256)
+        return make_error(CLAY_ERR_RECONSTRUCTION_FAILED, 0, 0, 0,
+                          "RS reconstruction failed: RS init failed: TooManyShards");
     erased.assign(c.q * c.t, 0);
     for (size_t i = 0; i < ner; i++) erased[internal_of(c, er[i])] = 1;
     *chunk_size = chunk;

@@ -21,6 +21,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -317,7 +318,11 @@ __global__ __launch_bounds__(kFusedBlock) void k_fused_encode(FusedArgs a, const
                               #expr);                                                                   \
     } while (0)
 
-static std::mutex g_mu;
+// Thread safety (include/clay.h): like the reference's immutable ClayCode (lib.rs:58),
+// every entry point may be called concurrently from any thread on any stream.  There
+// is no process-wide lock: the code/plan caches and the per-device pools each have
+// their own mutex, held only for lookups and bookkeeping, never across a launch or a
+// synchronisation of a caller's stream.
 static thread_local std::string t_last_path = "none";
 static thread_local size_t t_last_launches = 0;
 // Encode path selection (clay_set_encode_path): process-wide, read without locks.
@@ -342,29 +347,64 @@ static const DevProps &dev_props(int dev) {
     return g_props[dev];
 }
 
-struct Workspace {
-    void *ptr = nullptr;
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device)
+static Error lds_attr_once(const void *fn, int bytes, int dev) {
+    static std::mutex mu;
+    static std::set<std::pair<const void *, int>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({fn, dev})) return Error{};
+    CLAY_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.insert({fn, dev});
+    return Error{};
+}
+
+static bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// A pooled device buffer (U workspaces, host-API staging).  A lease is handed to one
+// call at a time; on release an event is recorded on the caller's stream, and the
+// buffer is handed out again only once that event has completed -- so streams that
+// come and go reuse the same few buffers instead of growing HBM per stream.  A lease
+// used inside a stream capture belongs to the captured graph for good (pinned).
+struct Lease {
+    void *d = nullptr;
     size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;  // stream of the last use (reuse there needs no event query)
+    bool used = false, busy = false, pinned = false;
 };
+// A batched launch's device pointer table, cached by content (immutable once
+// uploaded, so concurrent users may share it); freed LRU after its users' events.
+struct PtrTable {
+    void *d = nullptr;
+    void *h = nullptr;  // pinned source of the upload, kept: a captured copy node reads it
+    std::map<hipStream_t, hipEvent_t> evs;
+    uint64_t last = 0;
+    bool pinned = false;
+};
+constexpr size_t kMaxPtrTables = 64;
 
 struct DevState {
+    std::mutex mu;  // everything below
     bool init = false;
-    uint32_t *d_tabs = nullptr;                    // perm tables of all 256 constants
-    std::map<void *, Workspace> ws;                // per-stream U workspace
-    std::mutex host_mu;                            // serialises the host-buffer API per device
-    hipStream_t host_stream = nullptr;
-    Workspace host_bufs[3];
+    uint32_t *d_tabs = nullptr;                  // perm tables of all 256 constants
+    std::vector<std::unique_ptr<Lease>> pool;    // workspaces and staging buffers
+    std::map<std::vector<uint8_t *>, PtrTable> tables;
+    uint64_t tick = 0;
+    std::vector<hipStream_t> host_streams;       // idle streams of the host-buffer API
     // host-streaming pipeline (clay_encode_host_pipelined): streams + per-stream piece buffers
     std::mutex pipe_mu;
     std::vector<hipStream_t> pipe_streams;
-    std::vector<Workspace> pipe_bufs;
-    std::map<void *, Workspace> batch_tab;  // device pointer tables of batched launches, per stream
+    std::vector<Lease> pipe_bufs;
 };
 static DevState g_dev[64];
 
 struct CodeState {
     clay_code_t code{};
     RsCtx rs;
+    std::mutex mu;  // the plan maps, device uploads and mtab (plans are immutable once built)
     std::unique_ptr<Plan> enc;
     std::map<std::vector<uint8_t>, std::unique_ptr<Plan>> dec, rep;
     struct DevGrouped {
@@ -376,6 +416,7 @@ struct CodeState {
     std::map<int, uint32_t *> mtab;
     explicit CodeState(const clay_code_t &c) : code(c), rs(c) {}
 };
+static std::mutex g_codes_mu;
 static std::map<std::tuple<size_t, size_t, size_t>, std::unique_ptr<CodeState>> g_codes;
 
 struct DeviceGuard {
@@ -408,6 +449,7 @@ static Error dev_state(int dev, DevState **out) {
     if (dev < 0 || dev >= ndev || dev >= 64)
         return make_error(CLAY_ERR_DEVICE, size_t(dev), 0, 0, "HIP error: invalid device ordinal %d", dev);
     DevState &s = g_dev[dev];
+    std::lock_guard<std::mutex> lk(s.mu);
     if (!s.init) {
         DeviceGuard g(dev);
         std::vector<uint32_t> tabs(256 * 8);
@@ -421,6 +463,7 @@ static Error dev_state(int dev, DevState **out) {
 }
 
 static CodeState *code_state(const clay_code_t &c) {
+    std::lock_guard<std::mutex> lk(g_codes_mu);
     auto key = std::make_tuple(c.k, c.m, c.d);
     auto it = g_codes.find(key);
     if (it != g_codes.end()) return it->second.get();
@@ -428,6 +471,123 @@ static CodeState *code_state(const clay_code_t &c) {
     CodeState *p = cs.get();
     g_codes[key] = std::move(cs);
     return p;
+}
+
+// Idle pooled buffers beyond this many are freed when a new one is allocated.
+constexpr size_t kMaxIdleLeases = 4;
+
+static bool event_done(hipEvent_t ev) { return hipEventQuery(ev) == hipSuccess; }
+
+// Lease a device buffer of at least `bytes` for work on stream `st` (best fit among idle
+// buffers whose last use is complete or was on `st` itself; while `st` is capturing no
+// event is queried and nothing is freed).
+static Error lease_acquire(DevState &ds, size_t bytes, hipStream_t st, Lease **out) {
+    std::lock_guard<std::mutex> lk(ds.mu);
+    const bool cap = capturing(st);
+    Lease *best = nullptr;
+    for (auto &l : ds.pool) {
+        if (l->busy || l->pinned || l->bytes < bytes || (best && l->bytes >= best->bytes)) continue;
+        if (!l->used || l->last == st || (!cap && event_done(l->ev))) best = l.get();
+    }
+    if (!best && !cap) {
+        // free idle leases too small for this request, keeping the pool bounded
+        size_t idle = 0;
+        for (auto &l : ds.pool) idle += (!l->busy && !l->pinned);
+        for (auto it = ds.pool.begin(); it != ds.pool.end() && idle >= kMaxIdleLeases;) {
+            Lease &l = **it;
+            if (!l.busy && !l.pinned && l.bytes < bytes && hipEventSynchronize(l.ev) == hipSuccess) {
+                (void)hipFree(l.d);
+                (void)hipEventDestroy(l.ev);
+                it = ds.pool.erase(it);
+                idle--;
+            } else {
+                ++it;
+            }
+        }
+    }
+    if (!best) {
+        auto l = std::make_unique<Lease>();
+        CLAY_HIP(hipMalloc(&l->d, std::max<size_t>(bytes, 256)));
+        l->bytes = std::max<size_t>(bytes, 256);
+        CLAY_HIP(hipEventCreateWithFlags(&l->ev, hipEventDisableTiming));
+        best = l.get();
+        ds.pool.push_back(std::move(l));
+    }
+    // order after the previous user even if `st` is a recycled handle of a destroyed
+    // stream whose work is still running (free when that work is complete)
+    if (best->used && !cap) CLAY_HIP(hipStreamWaitEvent(st, best->ev, 0));
+    best->busy = true;
+    *out = best;
+    return Error{};
+}
+// Hand a lease back after its last use was enqueued on `st`.
+static void lease_release(DevState &ds, Lease *l, hipStream_t st) {
+    if (!l) return;
+    std::lock_guard<std::mutex> lk(ds.mu);
+    if (capturing(st)) {
+        l->pinned = true;
+    } else {
+        (void)hipEventRecord(l->ev, st);
+        l->last = st;
+        l->used = true;
+    }
+    l->busy = false;
+}
+struct LeaseGuard {
+    DevState &ds;
+    Lease *l = nullptr;
+    hipStream_t st;
+    LeaseGuard(DevState &d, hipStream_t s) : ds(d), st(s) {}
+    ~LeaseGuard() { lease_release(ds, l, st); }
+    uint8_t *ptr() const { return static_cast<uint8_t *>(l->d); }
+};
+
+// Device copy of a batched launch's pointer table: uploaded once per distinct table
+// (hipMemcpyAsync from pinned memory on `st`), then reused by every call with the same
+// buffers -- no per-call synchronisation or blocking copy, and graph-capture safe.
+static Error ptr_table(DevState &ds, const std::vector<uint8_t *> &tab, hipStream_t st, PtrTable **out) {
+    std::lock_guard<std::mutex> lk(ds.mu);
+    auto it = ds.tables.find(tab);
+    if (it == ds.tables.end()) {
+        if (ds.tables.size() >= kMaxPtrTables) {  // evict the least recently used unpinned table
+            auto victim = ds.tables.end();
+            for (auto j = ds.tables.begin(); j != ds.tables.end(); ++j)
+                if (!j->second.pinned && (victim == ds.tables.end() || j->second.last < victim->second.last)) victim = j;
+            if (victim != ds.tables.end()) {
+                for (auto &se : victim->second.evs) {
+                    (void)hipEventSynchronize(se.second);
+                    (void)hipEventDestroy(se.second);
+                }
+                (void)hipFree(victim->second.d);
+                (void)hipHostFree(victim->second.h);
+                ds.tables.erase(victim);
+            }
+        }
+        const size_t bytes = tab.size() * sizeof(uint8_t *);
+        PtrTable t;
+        CLAY_HIP(hipMalloc(&t.d, bytes));
+        CLAY_HIP(hipHostMalloc(&t.h, bytes, hipHostMallocDefault));
+        std::memcpy(t.h, tab.data(), bytes);
+        CLAY_HIP(hipMemcpyAsync(t.d, t.h, bytes, hipMemcpyHostToDevice, st));
+        it = ds.tables.emplace(tab, t).first;
+    }
+    it->second.last = ++ds.tick;
+    if (capturing(st)) it->second.pinned = true;
+    *out = &it->second;
+    return Error{};
+}
+// after the launches that read the table were enqueued on `st`
+static Error ptr_table_used(DevState &ds, PtrTable *t, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(ds.mu);
+    if (t->pinned) return Error{};
+    auto it = t->evs.find(st);
+    if (it == t->evs.end()) {
+        hipEvent_t ev;
+        CLAY_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        it = t->evs.emplace(st, ev).first;
+    }
+    CLAY_HIP(hipEventRecord(it->second, st));
+    return Error{};
 }
 
 template <typename T>
@@ -439,7 +599,9 @@ static Error upload_vec(const std::vector<T> &v, const T **out) {
     return Error{};
 }
 
+// Device copy of a plan's groups (once per plan and device; plans are never freed).
 static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::DevGrouped *out) {
+    std::lock_guard<std::mutex> lk(cs.mu);
     auto key = std::make_pair(&pl, dev);
     auto it = cs.gplan.find(key);
     if (it == cs.gplan.end()) {
@@ -452,6 +614,31 @@ static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::De
         it = cs.gplan.emplace(key, g).first;
     }
     *out = it->second;
+    return Error{};
+}
+
+// Cached plan lookup / build (plans are immutable once built).
+template <class Build>
+static Error cached_plan(CodeState &cs, std::map<std::vector<uint8_t>, std::unique_ptr<Plan>> &m,
+                         const std::vector<uint8_t> &key, Build &&build, const Plan **out) {
+    std::lock_guard<std::mutex> lk(cs.mu);
+    auto it = m.find(key);
+    if (it == m.end()) {
+        std::unique_ptr<Plan> p;
+        Error e = build(p);
+        if (e) return e;
+        it = m.emplace(key, std::move(p)).first;
+    }
+    *out = it->second.get();
+    return Error{};
+}
+static Error encode_plan(CodeState &cs, const Plan **out) {
+    std::lock_guard<std::mutex> lk(cs.mu);
+    if (!cs.enc) {
+        Error e = plan_encode(cs.code, cs.rs, cs.enc);
+        if (e) return e;
+    }
+    *out = cs.enc.get();
     return Error{};
 }
 
@@ -478,23 +665,6 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
         (ptab ? k_gexec<VW, 8, true> : k_gexec<VW, 8, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
 }
 
-
-static Error ensure_ws(DevState &ds, void *stream, size_t bytes, void **out) {
-    Workspace &w = ds.ws[stream];
-    if (w.bytes < bytes) {
-        if (w.ptr) {
-            CLAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-            CLAY_HIP(hipFree(w.ptr));
-            w.ptr = nullptr;
-            w.bytes = 0;
-        }
-        CLAY_HIP(hipMalloc(&w.ptr, bytes));
-        w.bytes = bytes;
-    }
-    *out = w.ptr;
-    return Error{};
-}
-
 static int align_of(uintptr_t p) {
     for (int a = 16; a > 1; a >>= 1)
         if ((p % a) == 0) return a;
@@ -505,16 +675,15 @@ static int align_of(uintptr_t p) {
 // launch per dependency level; 16 bytes per lane regardless of sc / pointer alignment.
 static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
                       ExecPtrs ptrs, size_t sc, size_t chunk_for_ws) {
-    Error e;
-    if (pl.uses_u) {
-        void *ws = nullptr;
-        e = ensure_ws(ds, stream, size_t(pl.tn) * chunk_for_ws, &ws);
-        if (e) return e;
-        ptrs.p[2 * pl.tn] = static_cast<uint8_t *>(ws);
-    }
     CodeState::DevGrouped g{};
-    e = upload_groups(cs, pl, dev, &g);
+    Error e = upload_groups(cs, pl, dev, &g);
     if (e) return e;
+    LeaseGuard ws(ds, stream);
+    if (pl.uses_u) {
+        e = lease_acquire(ds, size_t(pl.tn) * chunk_for_ws, stream, &ws.l);
+        if (e) return e;
+        ptrs.p[2 * pl.tn] = ws.ptr();
+    }
     size_t launches = 0;
     const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
     for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
@@ -541,12 +710,10 @@ static bool fused_shape_ok(const clay_code_t &c) {
 
 template <int Q, int PPT>
 static Error launch_fused(const FusedArgs &a, const uint32_t *mtab, size_t lds, hipStream_t stream, int grid) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fused_encode<Q, PPT>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(kFusedLdsBudget)));
-        attr_set = true;
-    }
+    int dev = 0;
+    CLAY_HIP(hipGetDevice(&dev));
+    Error e = lds_attr_once(reinterpret_cast<const void *>(&k_fused_encode<Q, PPT>), int(kFusedLdsBudget), dev);
+    if (e) return e;
     k_fused_encode<Q, PPT><<<dim3(grid), dim3(kFusedBlock), lds, stream>>>(a, mtab);
     CLAY_HIP(hipGetLastError());
     return Error{};
@@ -570,15 +737,20 @@ static Error encode_fused(CodeState &cs, DevState &ds, int dev, const uint8_t *c
     W = std::min<size_t>(W, 2048);
     if (W < size_t(ppt)) return Error{};
     // device RS parity rows as perm tables [p][i][8]
-    auto it = cs.mtab.find(dev);
-    if (it == cs.mtab.end()) {
-        std::vector<uint32_t> t(Q * K * 8);
-        for (size_t p = 0; p < Q; p++)
-            for (size_t i = 0; i < K; i++) perm_table(cs.rs.gen[(K + p) * K + i], &t[(p * K + i) * 8]);
-        uint32_t *d = nullptr;
-        CLAY_HIP(hipMalloc(&d, t.size() * 4));
-        CLAY_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
-        it = cs.mtab.emplace(dev, d).first;
+    const uint32_t *mt = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(cs.mu);
+        auto it = cs.mtab.find(dev);
+        if (it == cs.mtab.end()) {
+            std::vector<uint32_t> t(Q * K * 8);
+            for (size_t p = 0; p < Q; p++)
+                for (size_t i = 0; i < K; i++) perm_table(cs.rs.gen[(K + p) * K + i], &t[(p * K + i) * 8]);
+            uint32_t *d = nullptr;
+            CLAY_HIP(hipMalloc(&d, t.size() * 4));
+            CLAY_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+            it = cs.mtab.emplace(dev, d).first;
+        }
+        mt = it->second;
     }
     const hipDeviceProp_t &prop = dev_props(dev).raw;
     const size_t lds = Q * alpha * W;
@@ -602,15 +774,15 @@ static Error encode_fused(CodeState &cs, DevState &ds, int dev, const uint8_t *c
         const int grid = int(a.nslots * 8);
         Error e;
         switch (Q * 100 + ppt) {
-        case 216: e = launch_fused<2, 16>(a, it->second, lds, stream, grid); break;
-        case 208: e = launch_fused<2, 8>(a, it->second, lds, stream, grid); break;
-        case 204: e = launch_fused<2, 4>(a, it->second, lds, stream, grid); break;
-        case 316: e = launch_fused<3, 16>(a, it->second, lds, stream, grid); break;
-        case 308: e = launch_fused<3, 8>(a, it->second, lds, stream, grid); break;
-        case 304: e = launch_fused<3, 4>(a, it->second, lds, stream, grid); break;
-        case 416: e = launch_fused<4, 16>(a, it->second, lds, stream, grid); break;
-        case 408: e = launch_fused<4, 8>(a, it->second, lds, stream, grid); break;
-        case 404: e = launch_fused<4, 4>(a, it->second, lds, stream, grid); break;
+        case 216: e = launch_fused<2, 16>(a, mt, lds, stream, grid); break;
+        case 208: e = launch_fused<2, 8>(a, mt, lds, stream, grid); break;
+        case 204: e = launch_fused<2, 4>(a, mt, lds, stream, grid); break;
+        case 316: e = launch_fused<3, 16>(a, mt, lds, stream, grid); break;
+        case 308: e = launch_fused<3, 8>(a, mt, lds, stream, grid); break;
+        case 304: e = launch_fused<3, 4>(a, mt, lds, stream, grid); break;
+        case 416: e = launch_fused<4, 16>(a, mt, lds, stream, grid); break;
+        case 408: e = launch_fused<4, 8>(a, mt, lds, stream, grid); break;
+        case 404: e = launch_fused<4, 4>(a, mt, lds, stream, grid); break;
         default: return Error{};
         }
         if (e) return e;
@@ -672,14 +844,10 @@ static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_
         for (int i = 0; i < S::K; i++)
             if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
                 return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
     int dev = 0;
     CLAY_HIP(hipGetDevice(&dev));
-    if (!attr[dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[dev] = true;
-    }
+    Error ae = lds_attr_once(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS>), Kn::LDS_BYTES, dev);
+    if (ae) return ae;
     const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
     for (size_t s = 0; s < n_stripes; s++) {
         bs::BsArgs a{};
@@ -715,12 +883,8 @@ static Error launch_stream(CodeState &cs, const DevProps &prop, const uint8_t *c
         for (int i = 0; i < S::K; i++)
             if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
                 return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    static bool attr[64] = {};
-    if (!attr[prop.dev]) {
-        CLAY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_encode<KD, LOADERS>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES));
-        attr[prop.dev] = true;
-    }
+    Error ae = lds_attr_once(reinterpret_cast<const void *>(&bs::k_stream_encode<KD, LOADERS>), Kn::LDS_BYTES, prop.dev);
+    if (ae) return ae;
     // XCD region: sc / 8 rounded up to 32 bytes; one workgroup per CU
     const uint32_t region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
@@ -801,16 +965,15 @@ static Error encode_staged(CodeState &cs, DevState &ds, int dev, const uint8_t *
     const clay_code_t &c = cs.code;
     if (c.q * c.t > size_t(kMaxTn))
         return make_error(CLAY_ERR_DEVICE, c.q * c.t, 0, 0, "device engine supports at most %d internal nodes", kMaxTn);
-    if (!cs.enc) {
-        Error e = plan_encode(c, cs.rs, cs.enc);
-        if (e) return e;
-    }
+    const Plan *pl = nullptr;
+    Error pe = encode_plan(cs, &pl);
+    if (pe) return pe;
     const size_t sc = chunk / c.sub_chunk_no;
     for (size_t s = 0; s < n_stripes; s++) {
         ExecPtrs P{};
         for (size_t i = 0; i < c.k; i++) P.p[i] = const_cast<uint8_t *>(data[s * c.k + i]);
         for (size_t i = 0; i < c.m; i++) P.p[c.k + c.nu + i] = par[s * c.m + i];
-        Error e = run_plan(cs, *cs.enc, dev, ds, stream, P, sc, chunk);
+        Error e = run_plan(cs, *pl, dev, ds, stream, P, sc, chunk);
         if (e) return e;
     }
     t_last_path = "staged";
@@ -819,57 +982,54 @@ static Error encode_staged(CodeState &cs, DevState &ds, int dev, const uint8_t *
 
 // Batched small stripes: every level of the staged encode plan
 // runs for ALL stripes in one k_gexec launch (grid.y = stripe), pointers from a
-// device table of kMaxBases entries per stripe; U workspace per stripe.
+// cached device table of kMaxBases entries per stripe; U workspace per stripe.
+// At most kMaxBatch stripes per launch group (grid.y limit).
+constexpr size_t kMaxBatch = 65535;
 static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uint8_t *const *data,
                                  uint8_t *const *par, size_t n_stripes, size_t chunk, hipStream_t stream) {
     const clay_code_t &c = cs.code;
     const uint32_t tn = uint32_t(c.q * c.t);
-    if (!cs.enc) {
-        Error e = plan_encode(c, cs.rs, cs.enc);
-        if (e) return e;
-    }
-    const Plan &pl = *cs.enc;
-    CodeState::DevGrouped g{};
-    Error e = upload_groups(cs, pl, dev, &g);
+    const Plan *plp = nullptr;
+    Error e = encode_plan(cs, &plp);
     if (e) return e;
-    void *ws = nullptr;
-    if (pl.uses_u) {
-        e = ensure_ws(ds, stream, n_stripes * tn * chunk, &ws);
-        if (e) return e;
-    }
-    std::vector<uint8_t *> tab(n_stripes * kMaxBases, nullptr);
-    for (size_t s = 0; s < n_stripes; s++) {
-        uint8_t **t = &tab[s * kMaxBases];
-        for (size_t i = 0; i < c.k; i++) t[i] = const_cast<uint8_t *>(data[s * c.k + i]);
-        for (size_t i = 0; i < c.m; i++) t[c.k + c.nu + i] = par[s * c.m + i];
-        if (ws) t[2 * tn] = static_cast<uint8_t *>(ws) + s * tn * chunk;
-    }
-    // the table buffer is reused across calls: drain earlier batches on this stream first
-    Workspace &tb = ds.batch_tab[stream];
-    const size_t bytes = tab.size() * sizeof(uint8_t *);
-    CLAY_HIP(hipStreamSynchronize(stream));
-    if (tb.bytes < bytes) {
-        if (tb.ptr) CLAY_HIP(hipFree(tb.ptr));
-        tb.ptr = nullptr;
-        tb.bytes = 0;
-        CLAY_HIP(hipMalloc(&tb.ptr, bytes));
-        tb.bytes = bytes;
-    }
-    CLAY_HIP(hipMemcpy(tb.ptr, tab.data(), bytes, hipMemcpyHostToDevice));
+    const Plan &pl = *plp;
+    CodeState::DevGrouped g{};
+    e = upload_groups(cs, pl, dev, &g);
+    if (e) return e;
     const uint64_t sc = chunk / c.sub_chunk_no;
     const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
-    ExecPtrs P{};
     size_t launches = 0;
-    for (size_t st = 0; st + 1 < pl.gstage_begin.size(); st++) {
-        uint32_t b = pl.gstage_begin[st], end = pl.gstage_begin[st + 1];
-        while (b < end) {
-            uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
-            launch_gexec<16>(pl.gstage_maxd[st], dim3(n * tiles), stream, P, g, ds.d_tabs, b, tiles, sc, 0, sc, n,
-                             static_cast<uint8_t *const *>(tb.ptr), uint32_t(n_stripes));
-            CLAY_HIP(hipGetLastError());
-            launches++;
-            b += n;
+    for (size_t s0 = 0; s0 < n_stripes; s0 += kMaxBatch) {
+        const size_t ns = std::min(kMaxBatch, n_stripes - s0);
+        LeaseGuard ws(ds, stream);
+        if (pl.uses_u) {
+            e = lease_acquire(ds, ns * tn * chunk, stream, &ws.l);
+            if (e) return e;
         }
+        std::vector<uint8_t *> tab(ns * kMaxBases, nullptr);
+        for (size_t s = 0; s < ns; s++) {
+            uint8_t **t = &tab[s * kMaxBases];
+            for (size_t i = 0; i < c.k; i++) t[i] = const_cast<uint8_t *>(data[(s0 + s) * c.k + i]);
+            for (size_t i = 0; i < c.m; i++) t[c.k + c.nu + i] = par[(s0 + s) * c.m + i];
+            if (ws.l) t[2 * tn] = ws.ptr() + s * tn * chunk;
+        }
+        PtrTable *pt = nullptr;
+        e = ptr_table(ds, tab, stream, &pt);
+        if (e) return e;
+        ExecPtrs P{};
+        for (size_t st = 0; st + 1 < pl.gstage_begin.size(); st++) {
+            uint32_t b = pl.gstage_begin[st], end = pl.gstage_begin[st + 1];
+            while (b < end) {
+                uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
+                launch_gexec<16>(pl.gstage_maxd[st], dim3(n * tiles), stream, P, g, ds.d_tabs, b, tiles, sc, 0, sc, n,
+                                 static_cast<uint8_t *const *>(pt->d), uint32_t(ns));
+                CLAY_HIP(hipGetLastError());
+                launches++;
+                b += n;
+            }
+        }
+        e = ptr_table_used(ds, pt, stream);
+        if (e) return e;
     }
     t_last_launches += launches;
     t_last_path = "staged-batch";
@@ -888,7 +1048,6 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
         if (!data[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null data chunk");
     for (size_t i = 0; i < n_stripes * code->m; i++)
         if (!par[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk");
-    std::lock_guard<std::mutex> lk(g_mu);
     t_last_launches = 0;
     DevState *ds;
     e = dev_state(dev, &ds);
@@ -902,7 +1061,7 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
     const int mode = g_encode_mode.load(std::memory_order_relaxed), tile = g_encode_tile.load(std::memory_order_relaxed);
     // many small stripes: one launch per plan level for the whole batch instead of
     // one launch per stripe (launch-bound below ~4 MiB of data per stripe)
-    if (mode == kModeAuto && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) && n_stripes <= 65535 &&
+    if (mode == kModeAuto && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) &&
         code->q * code->t <= size_t(kMaxTn))
         return encode_staged_batch(cs, *ds, dev, data, par, n_stripes, chunk, st);
     if (mode == kModeAuto || mode >= kModeBs) {
@@ -951,7 +1110,6 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
                               er[i]);
         want[in] = outs[er[i]] ? 1 : 0;
     }
-    std::lock_guard<std::mutex> lk(g_mu);
     t_last_launches = 0;
     DevState *ds;
     e = dev_state(dev, &ds);
@@ -962,19 +1120,16 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         return make_error(CLAY_ERR_DEVICE, tn, 0, 0, "device engine supports at most %d internal nodes", kMaxTn);
     std::vector<uint8_t> key(erased);
     key.insert(key.end(), want.begin(), want.end());
-    auto it = cs.dec.find(key);
-    if (it == cs.dec.end()) {
-        std::unique_ptr<Plan> p;
-        e = plan_decode(c, cs.rs, erased, want, p);
-        if (e) return e;
-        it = cs.dec.emplace(key, std::move(p)).first;
-    }
+    const Plan *plan = nullptr;
+    e = cached_plan(cs, cs.dec, key, [&](std::unique_ptr<Plan> &p) { return plan_decode(c, cs.rs, erased, want, p); },
+                    &plan);
+    if (e) return e;
     ExecPtrs P{};
     for (size_t i = 0; i < c.n; i++) {
         size_t in = internal_of(c, i);
         P.p[in] = chunks[i] ? const_cast<uint8_t *>(chunks[i]) : (want[in] ? outs[i] : nullptr);
     }
-    return run_plan(cs, *it->second, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
+    return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
 }
 
 static Error repair_device_impl(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs,
@@ -989,7 +1144,6 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
     e = validate_repair(c, lost, ids, lens, nh, chunk, hin, slot_of, sub);
     if (e) return e;
     if (!out) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output");
-    std::lock_guard<std::mutex> lk(g_mu);
     t_last_launches = 0;
     DevState *ds;
     e = dev_state(dev, &ds);
@@ -1003,52 +1157,50 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
     key.push_back(uint8_t(lost & 0xFF));
     key.push_back(uint8_t(lost >> 8));
     key.push_back(uint8_t(full));
-    auto it = cs.rep.find(key);
-    if (it == cs.rep.end()) {
-        std::unique_ptr<Plan> p;
-        e = plan_repair(c, cs.rs, lost, hin, slot_of, sub, p, full);
-        if (e) return e;
-        it = cs.rep.emplace(key, std::move(p)).first;
-    }
+    const Plan *plan = nullptr;
+    e = cached_plan(cs, cs.rep, key,
+                    [&](std::unique_ptr<Plan> &p) { return plan_repair(c, cs.rs, lost, hin, slot_of, sub, p, full); },
+                    &plan);
+    if (e) return e;
     ExecPtrs P{};
     for (size_t in = 0; in < tn; in++)
         if (slot_of[in] >= 0) P.p[tn + in] = const_cast<uint8_t *>(bufs[slot_of[in]]);
     P.p[2 * tn + 1] = out;
-    return run_plan(cs, *it->second, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
+    return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
 }
 
 // ---------------------------------------------------------------------------
-// Host-buffer API helpers: device staging buffers per device.
+// Host-buffer API helpers: each call takes an idle stream of the current device
+// (created on demand) and pooled staging buffers, so host calls from different
+// threads run concurrently.
 // ---------------------------------------------------------------------------
-static Error host_buf(DevState &ds, int which, size_t bytes, uint8_t **out) {
-    Workspace &w = ds.host_bufs[which];
-    if (w.bytes < bytes) {
-        if (w.ptr) CLAY_HIP(hipFree(w.ptr));
-        w.ptr = nullptr;
-        w.bytes = 0;
-        CLAY_HIP(hipMalloc(&w.ptr, std::max<size_t>(bytes, 1)));
-        w.bytes = bytes;
+struct HostCall {
+    int dev = 0;
+    DevState *ds = nullptr;
+    hipStream_t st = nullptr;
+    ~HostCall() {
+        if (ds && st) {
+            std::lock_guard<std::mutex> lk(ds->mu);
+            ds->host_streams.push_back(st);
+        }
     }
-    *out = static_cast<uint8_t *>(w.ptr);
-    return Error{};
-}
-
-static Error host_device(int *dev, DevState **ds) {
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-        return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: no GPU device available (no CPU fallback)");
-    int d = 0;
-    (void)hipGetDevice(&d);
-    *dev = d;
-    Error e;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        e = dev_state(d, ds);
+    Error begin() {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: no GPU device available (no CPU fallback)");
+        (void)hipGetDevice(&dev);
+        Error e = dev_state(dev, &ds);
+        if (e) return e;
+        std::lock_guard<std::mutex> lk(ds->mu);
+        if (!ds->host_streams.empty()) {
+            st = ds->host_streams.back();
+            ds->host_streams.pop_back();
+        } else {
+            CLAY_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        }
+        return Error{};
     }
-    if (e) return e;
-    if (!(*ds)->host_stream) CLAY_HIP(hipStreamCreateWithFlags(&(*ds)->host_stream, hipStreamNonBlocking));
-    return Error{};
-}
+};
 
 }  // namespace clay
 
@@ -1152,14 +1304,65 @@ int clay_reserve_workspace(const clay_code_t *code, size_t chunk, int device, cl
     if (err) std::memset(err, 0, sizeof(*err));
     Error e = check_code(code);
     if (e) return report(e, err);
-    std::lock_guard<std::mutex> lk(g_mu);
     DevState *ds;
     e = dev_state(device, &ds);
     if (e) return report(e, err);
     DeviceGuard g(device);
-    void *p;
-    e = ensure_ws(*ds, nullptr, code->q * code->t * chunk, &p);
+    // an idle workspace lease any stream can take, plus the encode plan on the device
+    Lease *l = nullptr;
+    e = lease_acquire(*ds, code->q * code->t * chunk, nullptr, &l);
+    if (e) return report(e, err);
+    lease_release(*ds, l, nullptr);
+    CodeState &cs = *code_state(*code);
+    const Plan *pl = nullptr;
+    CodeState::DevGrouped gp{};
+    if (!cs.rs.init_err && code->q * code->t <= size_t(kMaxTn)) {
+        e = encode_plan(cs, &pl);
+        if (!e) e = upload_groups(cs, *pl, device, &gp);
+    }
     return e ? report(e, err) : 0;
+}
+
+int clay_release_workspace(int device, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    DevState *ds;
+    Error e = dev_state(device, &ds);
+    if (e) return report(e, err);
+    DeviceGuard g(device);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    for (auto it = ds->pool.begin(); it != ds->pool.end();) {
+        Lease &l = **it;
+        if (!l.busy && !l.pinned && hipEventSynchronize(l.ev) == hipSuccess) {
+            (void)hipFree(l.d);
+            (void)hipEventDestroy(l.ev);
+            it = ds->pool.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    for (auto it = ds->tables.begin(); it != ds->tables.end();) {
+        if (it->second.pinned) {
+            ++it;
+            continue;
+        }
+        for (auto &se : it->second.evs) {
+            (void)hipEventSynchronize(se.second);
+            (void)hipEventDestroy(se.second);
+        }
+        (void)hipFree(it->second.d);
+        (void)hipHostFree(it->second.h);
+        it = ds->tables.erase(it);
+    }
+    return 0;
+}
+
+size_t clay_workspace_bytes(int device) {
+    DevState *ds;
+    if (dev_state(device, &ds)) return 0;
+    std::lock_guard<std::mutex> lk(ds->mu);
+    size_t b = 0;
+    for (auto &l : ds->pool) b += l->bytes;
+    return b;
 }
 
 int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, const uint8_t *want, size_t lost,
@@ -1246,10 +1449,7 @@ int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *da
     const size_t np = (sc + w - 1) / w;
     const int ns = int(std::max<size_t>(1, std::min<size_t>(np, n_streams > 0 ? size_t(n_streams) : 2)));
     DevState *ds;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        e = dev_state(device, &ds);
-    }
+    e = dev_state(device, &ds);
     if (e) return report(e, err);
     std::lock_guard<std::mutex> pl(ds->pipe_mu);
     DeviceGuard g(device);
@@ -1265,15 +1465,15 @@ int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *da
     }
     const size_t need = (K + M) * alpha * w;
     for (int s = 0; s < ns; s++) {
-        Workspace &b = ds->pipe_bufs[s];
+        Lease &b = ds->pipe_bufs[s];
         if (b.bytes < need) {
-            if (b.ptr) {
+            if (b.d) {
                 if ((he = hipStreamSynchronize(ds->pipe_streams[s])) != hipSuccess) return fail(he);
-                if ((he = hipFree(b.ptr)) != hipSuccess) return fail(he);
-                b.ptr = nullptr;
+                if ((he = hipFree(b.d)) != hipSuccess) return fail(he);
+                b.d = nullptr;
                 b.bytes = 0;
             }
-            if ((he = hipMalloc(&b.ptr, need)) != hipSuccess) return fail(he);
+            if ((he = hipMalloc(&b.d, need)) != hipSuccess) return fail(he);
             b.bytes = need;
         }
     }
@@ -1283,7 +1483,7 @@ int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *da
     for (size_t p = 0; p < np; p++) {
         const int s = int(p % size_t(ns));
         hipStream_t st = ds->pipe_streams[s];
-        uint8_t *buf = static_cast<uint8_t *>(ds->pipe_bufs[s].ptr);
+        uint8_t *buf = static_cast<uint8_t *>(ds->pipe_bufs[s].d);
         const size_t off = p * w, wp = std::min(w, sc - off);
         for (size_t i = 0; i < K; i++) {
             uint8_t *dst = buf + i * alpha * wp;
@@ -1328,14 +1528,14 @@ int clay_encode(const clay_code_t *code, const uint8_t *data, size_t len, uint8_
         if (n) std::memcpy(out[i], data + lo, n);
         if (n < chunk) std::memset(out[i] + n, 0, chunk - n);
     }
-    int dev;
-    DevState *ds;
-    e = host_device(&dev, &ds);
-    if (e) return report(e, err);
-    std::lock_guard<std::mutex> hl(ds->host_mu);
-    uint8_t *d_data, *d_par;
-    if ((e = host_buf(*ds, 0, c.k * chunk, &d_data)) || (e = host_buf(*ds, 1, c.m * chunk, &d_par))) return report(e, err);
-    hipStream_t st = ds->host_stream;
+    HostCall hc;
+    if ((e = hc.begin())) return report(e, err);
+    const int dev = hc.dev;
+    hipStream_t st = hc.st;
+    LeaseGuard lin(*hc.ds, st), lout(*hc.ds, st);
+    if ((e = lease_acquire(*hc.ds, c.k * chunk, st, &lin.l)) || (e = lease_acquire(*hc.ds, c.m * chunk, st, &lout.l)))
+        return report(e, err);
+    uint8_t *d_data = lin.ptr(), *d_par = lout.ptr();
     auto fail = [&](hipError_t he) {
         return report(make_error(CLAY_ERR_DEVICE, size_t(he), 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
     };
@@ -1377,15 +1577,14 @@ int clay_decode(const clay_code_t *code, const size_t *ids, const uint8_t *const
     bool any_data_erased = false;
     for (size_t i = 0; i < ner; i++) any_data_erased |= er[i] < c.k;
     if (any_data_erased) {
-        int dev;
-        DevState *ds;
-        e = host_device(&dev, &ds);
-        if (e) return report(e, err);
-        std::lock_guard<std::mutex> hl(ds->host_mu);
-        uint8_t *d_in, *d_out;
-        if ((e = host_buf(*ds, 0, n_avail * chunk, &d_in)) || (e = host_buf(*ds, 1, c.k * chunk, &d_out)))
+        HostCall hc;
+        if ((e = hc.begin())) return report(e, err);
+        const int dev = hc.dev;
+        hipStream_t st = hc.st;
+        LeaseGuard lin(*hc.ds, st), lout(*hc.ds, st);
+        if ((e = lease_acquire(*hc.ds, n_avail * chunk, st, &lin.l)) || (e = lease_acquire(*hc.ds, c.k * chunk, st, &lout.l)))
             return report(e, err);
-        hipStream_t st = ds->host_stream;
+        uint8_t *d_in = lin.ptr(), *d_out = lout.ptr();
         std::vector<const uint8_t *> dch(c.n, nullptr);
         std::vector<uint8_t *> douts(c.n, nullptr);
         hipError_t he;
@@ -1424,15 +1623,15 @@ int clay_repair(const clay_code_t *code, size_t lost, const size_t *ids, const u
         if (e) return report(e, err);
     }
     if (!out) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output"), err);
-    int dev;
-    DevState *ds;
-    e = host_device(&dev, &ds);
-    if (e) return report(e, err);
-    std::lock_guard<std::mutex> hl(ds->host_mu);
+    HostCall hc;
+    if ((e = hc.begin())) return report(e, err);
+    const int dev = hc.dev;
+    hipStream_t st = hc.st;
     const size_t hb = lens[0];
-    uint8_t *d_in, *d_out;
-    if ((e = host_buf(*ds, 0, nh * hb, &d_in)) || (e = host_buf(*ds, 1, chunk, &d_out))) return report(e, err);
-    hipStream_t st = ds->host_stream;
+    LeaseGuard lin(*hc.ds, st), lout(*hc.ds, st);
+    if ((e = lease_acquire(*hc.ds, nh * hb, st, &lin.l)) || (e = lease_acquire(*hc.ds, chunk, st, &lout.l)))
+        return report(e, err);
+    uint8_t *d_in = lin.ptr(), *d_out = lout.ptr();
     std::vector<const uint8_t *> dh(nh);
     hipError_t he;
     for (size_t i = 0; i < nh; i++) {

@@ -15,7 +15,14 @@
  *     (ids[i], bufs[i], lens[i]); where the reference depends on HashMap
  *     iteration order (decode.rs:54-56, repair.rs:225) this ABI uses array order.
  *   - Thread safety: like the reference (ClayCode is immutable, lib.rs:58), all
- *     functions may be called concurrently; internal per-device caches are locked.
+ *     functions may be called concurrently, from any thread, on any stream.  There is
+ *     no process-wide lock: plan caches and per-device buffer pools are locked only
+ *     for bookkeeping, never across a launch or a wait on the caller's stream.
+ *   - Device buffers the library needs (U workspaces of decode/repair/staged encode,
+ *     staging buffers of the host API) come from a per-device pool; a buffer is reused
+ *     once the event recorded after its last use has completed, so streams that come
+ *     and go do not grow device memory.  Buffers and pointer tables first used inside
+ *     a stream capture stay reserved for the captured graph.
  *   - Host-buffer functions (clay_encode / clay_decode / clay_repair) copy to the
  *     GPU, run the HIP kernels and copy back.  *_device functions take device
  *     pointers and a hipStream_t (passed as void*) and are asynchronous.
@@ -32,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CLAY_ABI_VERSION 2
+#define CLAY_ABI_VERSION 3
 
 /* ClayCode public fields (lib.rs:59-82) + the two private RS counts (lib.rs:79-81). */
 typedef struct clay_code {
@@ -180,10 +187,19 @@ int clay_repair_device_full_chunks(const clay_code_t *code, size_t lost_node, co
 /* Engine control / introspection                                      */
 /* ------------------------------------------------------------------ */
 
-/* Pre-allocate per-device workspace for chunk_size (avoids allocation inside a
- * later call, e.g. before stream capture). */
+/* Pre-allocate an idle pooled workspace for chunk_size (any stream may take it) and
+ * build + upload the code's encode plan, so that a later call allocates nothing --
+ * e.g. before stream capture.  Decode/repair plans depend on the erasure pattern:
+ * run one call per pattern before capturing it. */
 int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int device,
                            clay_error_t *err);
+
+/* Free the device's idle pooled buffers (waiting for their last users' events) and
+ * its unpinned batch pointer tables.  Buffers in use or owned by captured graphs stay. */
+int clay_release_workspace(int device, clay_error_t *err);
+
+/* Bytes of device memory held by the device's buffer pool (tests / monitoring). */
+size_t clay_workspace_bytes(int device);
 
 /* Encode path selection (process-wide; tests and benchmarks).  Low byte = path:
  *   0 auto      -- the streaming kernel for q = 4, t = 4 codes with k = 9 / 10 (the

@@ -51,7 +51,7 @@ def test_library_is_gfx950_hip_binary():
     path = _lib.LIB_PATH
     blob = open(path, "rb").read()
     assert b"gfx950" in blob, "no gfx950 code object in libclay_amd.so"
-    assert _lib.lib().clay_abi_version() == 2
+    assert _lib.lib().clay_abi_version() == 3
 
 
 def test_library_ships_only_parity_producing_kernels():

@@ -1,0 +1,194 @@
+"""GPU runtime behaviour of the C ABI (include/clay.h): concurrency, the device buffer
+pool, graph capture and very large batches.  Every result is compared with the oracle.
+
+The reference's ClayCode is immutable and freely shareable across threads (lib.rs:58);
+the ABI promises the same: no process-wide lock, any thread, any stream."""
+import threading
+
+import numpy as np
+import pytest
+
+import clay_amd
+from clay_amd import ClayCode
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_bytes(seed, n):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def _stripe(o, k, chunk, seed):
+    return o.encode_array(rand_bytes(seed, k * chunk))
+
+
+def test_threads_and_streams_interleaved(oracle_mod, torch_cuda):
+    """2 host threads x 2 streams each, interleaving device encode, 4-erasure decode and
+    repair of (10,4,13) stripes, all in flight together; every output bit-exact."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    sc = 4104  # ragged tiles (sc % 16 == 8)
+    chunk = c.sub_chunk_no * sc
+    refs = [_stripe(o, 10, chunk, 7000 + i) for i in range(4)]
+    er = [0, 4, 8, 12]
+    lost = 2
+    info = c.minimum_to_repair(lost, [i for i in range(14) if i != lost])
+    errors = []
+
+    def worker(t):
+        try:
+            streams = [torch.cuda.Stream() for _ in range(2)]
+            jobs = []
+            for it in range(6):
+                st = streams[it % 2]
+                ref = refs[(t * 2 + it) % 4]
+                with torch.cuda.stream(st):
+                    full = torch.from_numpy(ref).cuda(non_blocking=False)
+                    par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
+                    c.encode_device([full[i] for i in range(10)], [par[i] for i in range(4)], chunk, 0,
+                                    st.cuda_stream)
+                    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+                    c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                                    [outs[i] if i in er else None for i in range(14)], chunk, 0, st.cuda_stream)
+                    rep = torch.zeros(chunk, dtype=torch.uint8, device="cuda")
+                    c.repair_device_full_chunks(lost, [h for h, _ in info], [full[h] for h, _ in info], chunk, rep,
+                                                0, st.cuda_stream)
+                jobs.append((st, ref, par, outs, rep))
+            for st, ref, par, outs, rep in jobs:
+                st.synchronize()
+                assert np.array_equal(par.cpu().numpy(), ref[10:]), "encode"
+                for e in er:
+                    assert np.array_equal(outs[e].cpu().numpy(), ref[e]), ("decode", e)
+                assert np.array_equal(rep.cpu().numpy(), ref[lost]), "repair"
+        except Exception as ex:  # noqa: BLE001 -- reported by the main thread
+            errors.append((t, repr(ex)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+
+
+def test_host_api_concurrent_threads(oracle_mod, torch_cuda):
+    """Host-buffer encode / decode from 3 threads at once (each call takes its own pooled
+    stream and staging buffers)."""
+    c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
+    datas = [bytes(rand_bytes(8100 + t, 9 * 81 * 2 * 37 + t)) for t in range(3)]
+    refs = [o.encode(d) for d in datas]
+    errors = []
+
+    def worker(t):
+        try:
+            for _ in range(4):
+                got = c.encode(datas[t])
+                assert got == refs[t]
+                av = {i: got[i] for i in range(12) if i not in (1, 10)}
+                assert c.decode(av, [1, 10]) == o.decode(av, [1, 10])
+        except Exception as ex:  # noqa: BLE001
+            errors.append((t, repr(ex)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+
+
+def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda):
+    """Decodes on 8 distinct, short-lived streams one after another reuse the pooled U
+    workspace: the pool does not grow per stream (it grew by one workspace per stream
+    handle before the pool existed)."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    sc = 1024
+    chunk = c.sub_chunk_no * sc
+    ref = _stripe(o, 10, chunk, 99)
+    full = torch.from_numpy(ref).cuda()
+    er = [1, 5]
+    clay_amd.release_workspace(0)
+    sizes = []
+    for i in range(8):
+        st = torch.cuda.Stream()
+        outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+        c.decode_device([None if j in er else full[j] for j in range(14)], er,
+                        [outs[j] if j in er else None for j in range(14)], chunk, 0, st.cuda_stream)
+        st.synchronize()
+        for e in er:
+            assert np.array_equal(outs[e].cpu().numpy(), ref[e])
+        sizes.append(clay_amd.workspace_bytes(0))
+        del st
+    assert sizes[0] >= 16 * chunk  # one U workspace (q t = 16 nodes)
+    assert sizes[-1] == sizes[0], sizes
+    clay_amd.release_workspace(0)
+    assert clay_amd.workspace_bytes(0) == 0
+
+
+def test_reserve_then_no_growth(oracle_mod, torch_cuda):
+    """clay_reserve_workspace leaves an idle workspace any stream can take."""
+    torch = torch_cuda
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    chunk = c.sub_chunk_no * 4096
+    clay_amd.release_workspace(0)
+    c.reserve_workspace(chunk)
+    reserved = clay_amd.workspace_bytes(0)
+    assert reserved >= c.q * c.t * chunk
+    ref = _stripe(o, 4, chunk, 5)
+    full = torch.from_numpy(ref).cuda()
+    st = torch.cuda.Stream()
+    outs = torch.zeros((6, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if j == 0 else full[j] for j in range(6)], [0], [outs[0]] + [None] * 5, chunk, 0,
+                    st.cuda_stream)
+    st.synchronize()
+    assert np.array_equal(outs[0].cpu().numpy(), ref[0])
+    assert clay_amd.workspace_bytes(0) == reserved
+
+
+def test_batch_encode_graph_capture(oracle_mod, torch_cuda):
+    """Batched small-stripe encode captured into a HIP graph and replayed on new data:
+    the pointer table is uploaded once from pinned memory (no blocking copy, no stream
+    sync inside the call), so the call is capturable."""
+    torch = torch_cuda
+    k, m, d = 4, 2, 5
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    n, chunk = 16, c.sub_chunk_no * 512
+    data = torch.zeros((n * k, chunk), dtype=torch.uint8, device="cuda")
+    par = torch.zeros((n * m, chunk), dtype=torch.uint8, device="cuda")
+    dl, pl = [data[i] for i in range(n * k)], [par[i] for i in range(n * m)]
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):  # warm-up outside capture: plan upload, workspace
+        c.encode_device_batch(dl, pl, n, chunk, 0, st.cuda_stream)
+    st.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        c.encode_device_batch(dl, pl, n, chunk, 0, torch.cuda.current_stream().cuda_stream)
+    for rep in range(2):
+        refs = [_stripe(o, k, chunk, 300 + 10 * rep + s) for s in range(n)]
+        data.copy_(torch.from_numpy(np.concatenate([r[:k] for r in refs])))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        got = par.cpu().numpy()
+        for s in range(n):
+            assert np.array_equal(got[s * m:(s + 1) * m], refs[s][k:]), (rep, s)
+
+
+def test_batch_encode_more_than_grid_y_limit(oracle_mod, torch_cuda):
+    """70,000 (4,2,5) 1 KiB-class stripes in one call: split into launch groups of at
+    most 65,535 stripes (the grid.y limit); stripes either side of the split match."""
+    torch = torch_cuda
+    k, m, d = 4, 2, 5
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    n, chunk = 70000, c.sub_chunk_no * 32  # sc 32 -> 256-byte chunks, 1 KiB of data per stripe
+    host = rand_bytes(4242, n * k * chunk).reshape(n * k, chunk)
+    data = torch.from_numpy(host).cuda()
+    par = torch.zeros((n * m, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device_batch([data[i] for i in range(n * k)], [par[i] for i in range(n * m)], n, chunk)
+    torch.cuda.synchronize()
+    assert clay_amd.last_encode_path() == "staged-batch"
+    got = par.cpu().numpy()
+    for s in (0, 1, 65534, 65535, 65536, n - 1):
+        ref = o.encode_array(host[s * k:(s + 1) * k].reshape(-1))
+        assert np.array_equal(got[s * m:(s + 1) * m], ref[k:]), s

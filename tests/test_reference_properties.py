@@ -233,3 +233,19 @@ def test_product_repair_validation_matches(oracle_mod):
             a.repair(lost, hd, cs)
         assert pe.value.kind == oe.value.kind and pe.value.fields == oe.value.fields
         assert str(pe.value) == oe.value.msg
+
+
+def test_product_decode_rs_shard_limit_matches(oracle_mod):
+    """(1,256,256): q = 256, original_count + recovery_count = 512 > 256.  decode_layered
+    builds ReedSolomon::new before any layer work (decode.rs:175-180), so even a decode with
+    no data node erased fails with ReconstructionFailed("RS init failed: TooManyShards")."""
+    a, b = ClayCode(1, 256, 256), oc(oracle_mod, 1, 256, 256)
+    chunk = a.sub_chunk_no  # 65,536: the smallest valid chunk
+    av = {i: bytes(chunk) for i in range(1, a.n)}
+    for er in ([0], []):
+        avail = av if er else {**av, 0: bytes(chunk)}
+        with pytest.raises(oracle_mod.OracleError) as oe:
+            b.decode(avail, er)
+        with pytest.raises(clay_amd.ClayError) as pe:
+            a.decode(avail, er)
+        assert pe.value.kind == oe.value.kind and str(pe.value) == oe.value.msg
