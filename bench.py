@@ -228,20 +228,20 @@ def small_stripe_rates(torch, dev, local, sh):
     from clay_amd import ClayCode
     import clay_amd
     code = ClayCode(4, 2, 5)
-    out = {"config": "(k=4,m=2,d=5) clay_encode_device_batch, ~64 MiB of input per call", "unit": "GiB/s"}
+    out = {"config": "(k=4,m=2,d=5) clay_encode_device_strided ([n][k][chunk] buffers), ~64 MiB of input per call",
+           "unit": "GiB/s"}
     for size in (1024, 10 * 1024, 100 * 1024, 1 << 20):
         chunk = code.encoded_chunk_size(size)
         n = max(4, (64 << 20) // (4 * chunk))
         data = torch.randint(0, 256, (n * 4, chunk), dtype=torch.uint8, device=dev)
         par = torch.empty((n * 2, chunk), dtype=torch.uint8, device=dev)
-        dp, pp = [data[i] for i in range(n * 4)], [par[i] for i in range(n * 2)]
         for _ in range(3):
-            code.encode_device_batch(dp, pp, n, chunk, local, sh)
+            code.encode_device_strided(data, par, n, chunk, device=local, stream=sh)
         torch.cuda.synchronize(dev)
         reps = 10
         t0 = time.perf_counter()
         for _ in range(reps):
-            code.encode_device_batch(dp, pp, n, chunk, local, sh)
+            code.encode_device_strided(data, par, n, chunk, device=local, stream=sh)
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
         out[f"{size}B"] = {"stripes_per_call": n, "GiBps": round(reps * n * size / el / 2**30, 2),

@@ -257,6 +257,23 @@ class ClayCode:
         if rc:
             _raise(rc, err)
 
+    def encode_device_strided(self, data, parity, n_stripes: int, chunk_size: int, data_node_stride: int = 0,
+                              data_stripe_stride: int = 0, parity_node_stride: int = 0,
+                              parity_stripe_stride: int = 0, device: int = 0, stream: int = 0):
+        """Batched encode of stripes at fixed strides (clay.h clay_encode_device_strided).
+        Strides default to a contiguous [n_stripes][k or m][chunk_size] layout."""
+        dns = data_node_stride or chunk_size
+        dss = data_stripe_stride or self.k * chunk_size
+        pns = parity_node_stride or chunk_size
+        pss = parity_stripe_stride or self.m * chunk_size
+        err = ClayErrorStruct()
+        rc = _lib.lib().clay_encode_device_strided(C.byref(self._c), C.c_void_p(_ptr(data)), dns, dss,
+                                                   C.c_void_p(_ptr(parity)), pns, pss, int(n_stripes),
+                                                   int(chunk_size), int(device), C.c_void_p(int(stream)),
+                                                   C.byref(err))
+        if rc:
+            _raise(rc, err)
+
     def reserve_workspace(self, chunk_size: int, device: int = 0):
         """Pre-allocate a pooled workspace and upload the encode plan (clay.h)."""
         err = ClayErrorStruct()

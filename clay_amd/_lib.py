@@ -52,6 +52,8 @@ SIGNATURES = {
                                                  C.c_int, _vp, _err_p]),
     "clay_reserve_workspace": (C.c_int, [_code_p, _sz, C.c_int, _err_p]),
     "clay_release_workspace": (C.c_int, [C.c_int, _err_p]),
+    "clay_encode_device_strided": (C.c_int, [_code_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                             C.c_int64, _sz, _sz, C.c_int, C.c_void_p, _err_p]),
     "clay_workspace_bytes": (_sz, [C.c_int]),
     "clay_plan_export": (C.c_int, [_code_p, C.c_int, _u8p, _u8p, _sz, _P(C.c_uint32), _sz,
                                    _P(C.c_uint32), _sz, _P(C.c_uint32), _sz, _P(_sz), _err_p]),

@@ -47,11 +47,18 @@ constexpr size_t kFusedLdsBudget = 128 * 1024;
 struct ExecPtrs {
     uint8_t *p[kMaxBases];
 };
+// Affine batches: region base b of stripe s is p[b] + s * stride[b] (bytes).
+struct ExecStride {
+    int64_t s[kMaxBases];
+};
+// k_gexec operand addressing: one stripe (kernarg pointers), a batch through a device
+// pointer table, or an affine batch (kernarg base + stripe * stride).
+enum : int { kBatchNone = 0, kBatchTable = 1, kBatchAffine = 2 };
 
 // Grouped staged executor: one workgroup = one source-sharing op group x one tile.
 // Each source tile is loaded once, split into its perm-table indices once, and
 // multiplied into up to MAXD destination accumulators (dst_d = XOR_s coef[d][s] * src_s).
-template <int VW, int MAXD, bool BATCH = false>
+template <int VW, int MAXD, int BATCH = kBatchNone>
 __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup *__restrict__ groups,
                                                       const DevSrc *__restrict__ gsrcs,
                                                       const DevSrc *__restrict__ gdsts,
@@ -59,7 +66,8 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                                                       const uint32_t *__restrict__ tabs, uint32_t g0,
                                                       uint32_t tiles, uint64_t sc, uint64_t r0, uint64_t r1,
                                                       uint32_t ngroups, uint32_t order, uint32_t bx,
-                                                      uint8_t *const *__restrict__ ptab) {
+                                                      uint8_t *const *__restrict__ ptab, uint32_t lps,
+                                                      uint32_t nstripes, const ExecStride S) {
     constexpr int NW = (VW + 3) / 4;
     // Block -> (group, tile).  order 0: group-major.  1: tile-major -- all groups of a
     // tile run back to back, so an input sub-chunk tile read by several groups is
@@ -78,8 +86,17 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
         tile = v / ngroups;
         gi = v - tile * ngroups;
     }
+    // BATCH: lps lanes per stripe; a block runs kExecBlock / lps stripes (small sub-chunks
+    // fill the block with stripes instead of idle lanes)
+    uint32_t lane = threadIdx.x, stripe = 0;
+    if constexpr (BATCH != kBatchNone) {
+        const uint32_t spb = kExecBlock / lps;
+        stripe = blockIdx.y * spb + threadIdx.x / lps;
+        lane = threadIdx.x % lps;
+        if (threadIdx.x >= spb * lps || stripe >= nstripes) return;
+    }
     const DevGroup g = groups[g0 + gi];
-    const uint64_t pos = r0 + (uint64_t(tile) * kExecBlock + threadIdx.x) * VW;
+    const uint64_t pos = r0 + (uint64_t(tile) * lps + lane) * VW;
     if (pos >= r1) return;
     // Regions start at slot*sc, which is only 2-byte aligned for e.g. the (9,3,11)
     // chunk of 268,435,458 B; gfx950 global loads/stores run in unaligned mode, so
@@ -104,8 +121,10 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                 const DevSrc src = gsrcs[g.src_begin + s];
                 // BATCH (template, so the single-stripe kernel keeps its kernarg pointer table)
                 const uint8_t *sp;
-                if constexpr (BATCH)
-                    sp = ptab[blockIdx.y * kMaxBases + src.base] + uint64_t(src.slot) * sc + pos;
+                if constexpr (BATCH == kBatchTable)
+                    sp = ptab[stripe * kMaxBases + src.base] + uint64_t(src.slot) * sc + pos;
+                else if constexpr (BATCH == kBatchAffine)
+                    sp = P.p[src.base] + int64_t(stripe) * S.s[src.base] + uint64_t(src.slot) * sc + pos;
                 else
                     sp = P.p[src.base] + uint64_t(src.slot) * sc + pos;
                 if (full) {
@@ -144,8 +163,10 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
         if (d >= int(g.ndst)) break;
         const DevSrc dst = gdsts[g.dst_begin + d];
         uint8_t *dp;
-        if constexpr (BATCH)
-            dp = ptab[blockIdx.y * kMaxBases + dst.base] + uint64_t(dst.slot) * sc + pos;
+        if constexpr (BATCH == kBatchTable)
+            dp = ptab[stripe * kMaxBases + dst.base] + uint64_t(dst.slot) * sc + pos;
+        else if constexpr (BATCH == kBatchAffine)
+            dp = P.p[dst.base] + int64_t(stripe) * S.s[dst.base] + uint64_t(dst.slot) * sc + pos;
         else
             dp = P.p[dst.base] + uint64_t(dst.slot) * sc + pos;
         if (full) {
@@ -642,27 +663,37 @@ static Error encode_plan(CodeState &cs, const Plan **out) {
     return Error{};
 }
 
+template <int VW, int MAXD>
+static void launch_gexec1(int mode, dim3 grid, dim3 block, hipStream_t stream, const ExecPtrs &ptrs,
+                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
+                          uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n, uint32_t order, uint32_t bx,
+                          uint8_t *const *ptab, uint32_t lps, uint32_t nstripes, const ExecStride &S) {
+    auto k = mode == kBatchTable ? k_gexec<VW, MAXD, kBatchTable>
+           : mode == kBatchAffine ? k_gexec<VW, MAXD, kBatchAffine> : k_gexec<VW, MAXD, kBatchNone>;
+    k<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx,
+                                  ptab, lps, nstripes, S);
+}
 template <int VW>
 static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
-                         uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n, uint8_t *const *ptab = nullptr,
-                         uint32_t nstripes = 1) {
+                         uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n, int mode = kBatchNone,
+                         uint8_t *const *ptab = nullptr, const ExecStride *stride = nullptr, uint32_t nstripes = 1,
+                         uint32_t lps = kExecBlock) {
     dim3 block(kExecBlock);
     static const uint32_t order = [] {
         const char *e = getenv("CLAY_GEXEC_ORDER");
         return e ? uint32_t(atoi(e)) : 2u;
     }();
+    static const ExecStride zero{};
+    const ExecStride &S = stride ? *stride : zero;
     const uint32_t nb = n * tiles, bx = (nb + 7) / 8;
     if (order == 2) grid = dim3(8 * bx);
-    grid.y = nstripes;
-    if (maxd <= 1)
-        (ptab ? k_gexec<VW, 1, true> : k_gexec<VW, 1, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
-    else if (maxd <= 2)
-        (ptab ? k_gexec<VW, 2, true> : k_gexec<VW, 2, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
-    else if (maxd <= 4)
-        (ptab ? k_gexec<VW, 4, true> : k_gexec<VW, 4, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
-    else
-        (ptab ? k_gexec<VW, 8, true> : k_gexec<VW, 8, false>)<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab);
+    const uint32_t spb = kExecBlock / lps;
+    grid.y = (nstripes + spb - 1) / spb;
+    if (maxd <= 1) launch_gexec1<VW, 1>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
+    else if (maxd <= 2) launch_gexec1<VW, 2>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
+    else if (maxd <= 4) launch_gexec1<VW, 4>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
+    else launch_gexec1<VW, 8>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
 }
 
 static int align_of(uintptr_t p) {
@@ -983,10 +1014,20 @@ static Error encode_staged(CodeState &cs, DevState &ds, int dev, const uint8_t *
 // Batched small stripes: every level of the staged encode plan
 // runs for ALL stripes in one k_gexec launch (grid.y = stripe), pointers from a
 // cached device table of kMaxBases entries per stripe; U workspace per stripe.
-// At most kMaxBatch stripes per launch group (grid.y limit).
-constexpr size_t kMaxBatch = 65535;
+// Sub-chunks under 4 KiB put several stripes in one block (lps lanes of 16 B per
+// stripe); at most 65,535 blocks of stripes per launch group (grid.y limit).
+// Stripes laid out at fixed strides (clay_encode_device_strided): node i of stripe s at
+// data + s * dstripe + i * dnode, parity j at par + s * pstripe + j * pnode.
+struct Strided {
+    const uint8_t *data;
+    int64_t dnode, dstripe;
+    uint8_t *par;
+    int64_t pnode, pstripe;
+};
+
 static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uint8_t *const *data,
-                                 uint8_t *const *par, size_t n_stripes, size_t chunk, hipStream_t stream) {
+                                 uint8_t *const *par, size_t n_stripes, size_t chunk, hipStream_t stream,
+                                 const Strided *sd) {
     const clay_code_t &c = cs.code;
     const uint32_t tn = uint32_t(c.q * c.t);
     const Plan *plp = nullptr;
@@ -997,39 +1038,76 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
     e = upload_groups(cs, pl, dev, &g);
     if (e) return e;
     const uint64_t sc = chunk / c.sub_chunk_no;
-    const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+    const uint32_t lanes = uint32_t(sc / 16 + 1);  // 16-byte lanes incl. the byte tail
+    const uint32_t lps = std::min<uint32_t>(kExecBlock, lanes);
+    const uint32_t tiles = (lanes + lps - 1) / lps;
+    const size_t max_group = size_t(65535) * (kExecBlock / lps);
     size_t launches = 0;
-    for (size_t s0 = 0; s0 < n_stripes; s0 += kMaxBatch) {
-        const size_t ns = std::min(kMaxBatch, n_stripes - s0);
+    for (size_t s0 = 0; s0 < n_stripes; s0 += max_group) {
+        const size_t ns = std::min(max_group, n_stripes - s0);
         LeaseGuard ws(ds, stream);
         if (pl.uses_u) {
             e = lease_acquire(ds, ns * tn * chunk, stream, &ws.l);
             if (e) return e;
         }
-        std::vector<uint8_t *> tab(ns * kMaxBases, nullptr);
-        for (size_t s = 0; s < ns; s++) {
-            uint8_t **t = &tab[s * kMaxBases];
-            for (size_t i = 0; i < c.k; i++) t[i] = const_cast<uint8_t *>(data[(s0 + s) * c.k + i]);
-            for (size_t i = 0; i < c.m; i++) t[c.k + c.nu + i] = par[(s0 + s) * c.m + i];
-            if (ws.l) t[2 * tn] = ws.ptr() + s * tn * chunk;
+        // operand of base b for stripe s: affine in s (rows of one buffer, the common
+        // case) -> kernarg base + stride, no table; otherwise a cached device table
+        ExecPtrs P{};
+        ExecStride S{};
+        bool affine = true;
+        auto affine_of = [&](size_t base, auto ptr_of) {
+            if (sd) {  // strided layout: affine by construction
+                P.p[base] = ptr_of(0);
+                S.s[base] = int64_t(ptr_of(1) - ptr_of(0));
+                return;
+            }
+            uint8_t *p0 = ptr_of(0);
+            const int64_t st = ns > 1 ? int64_t(ptr_of(1) - p0) : 0;
+            for (size_t s = 2; s < ns && affine; s++) affine = ptr_of(s) == p0 + int64_t(s) * st;
+            P.p[base] = p0;
+            S.s[base] = st;
+        };
+        for (size_t i = 0; i < c.k && affine; i++)
+            affine_of(i, [&](size_t s) {
+                return sd ? const_cast<uint8_t *>(sd->data) + int64_t(s0 + s) * sd->dstripe + int64_t(i) * sd->dnode
+                          : const_cast<uint8_t *>(data[(s0 + s) * c.k + i]);
+            });
+        for (size_t i = 0; i < c.m && affine; i++)
+            affine_of(c.k + c.nu + i, [&](size_t s) {
+                return sd ? sd->par + int64_t(s0 + s) * sd->pstripe + int64_t(i) * sd->pnode : par[(s0 + s) * c.m + i];
+            });
+        if (ws.l) {
+            P.p[2 * tn] = ws.ptr();
+            S.s[2 * tn] = int64_t(tn * chunk);
         }
         PtrTable *pt = nullptr;
-        e = ptr_table(ds, tab, stream, &pt);
-        if (e) return e;
-        ExecPtrs P{};
+        if (!affine) {
+            std::vector<uint8_t *> tab(ns * kMaxBases, nullptr);
+            for (size_t s = 0; s < ns; s++) {
+                uint8_t **t = &tab[s * kMaxBases];
+                for (size_t i = 0; i < c.k; i++) t[i] = const_cast<uint8_t *>(data[(s0 + s) * c.k + i]);
+                for (size_t i = 0; i < c.m; i++) t[c.k + c.nu + i] = par[(s0 + s) * c.m + i];
+                if (ws.l) t[2 * tn] = ws.ptr() + s * tn * chunk;
+            }
+            e = ptr_table(ds, tab, stream, &pt);
+            if (e) return e;
+        }
         for (size_t st = 0; st + 1 < pl.gstage_begin.size(); st++) {
             uint32_t b = pl.gstage_begin[st], end = pl.gstage_begin[st + 1];
             while (b < end) {
                 uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
                 launch_gexec<16>(pl.gstage_maxd[st], dim3(n * tiles), stream, P, g, ds.d_tabs, b, tiles, sc, 0, sc, n,
-                                 static_cast<uint8_t *const *>(pt->d), uint32_t(ns));
+                                 affine ? kBatchAffine : kBatchTable,
+                                 pt ? static_cast<uint8_t *const *>(pt->d) : nullptr, &S, uint32_t(ns), lps);
                 CLAY_HIP(hipGetLastError());
                 launches++;
                 b += n;
             }
         }
-        e = ptr_table_used(ds, pt, stream);
-        if (e) return e;
+        if (pt) {
+            e = ptr_table_used(ds, pt, stream);
+            if (e) return e;
+        }
     }
     t_last_launches += launches;
     t_last_path = "staged-batch";
@@ -1037,17 +1115,21 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
 }
 
 static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *data, uint8_t *const *par,
-                                size_t n_stripes, size_t chunk, int dev, void *stream) {
+                                size_t n_stripes, size_t chunk, int dev, void *stream, const Strided *sd = nullptr) {
     Error e = check_code(code);
     if (e) return e;
-    if (!data || !par) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null chunk array");
+    if (sd ? (!sd->data || !sd->par) : (!data || !par))
+        return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null chunk array");
     if (chunk == 0 || chunk % code->sub_chunk_no != 0)
         return make_error(CLAY_ERR_INVALID_CHUNK_SIZE, code->sub_chunk_no, chunk, 0,
                           "Invalid chunk size: expected divisible by %zu, got %zu", code->sub_chunk_no, chunk);
-    for (size_t i = 0; i < n_stripes * code->k; i++)
-        if (!data[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null data chunk");
-    for (size_t i = 0; i < n_stripes * code->m; i++)
-        if (!par[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk");
+    if (!sd) {
+        for (size_t i = 0; i < n_stripes * code->k; i++)
+            if (!data[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null data chunk");
+        for (size_t i = 0; i < n_stripes * code->m; i++)
+            if (!par[i]) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk");
+    }
+    if (n_stripes == 0) return Error{};
     t_last_launches = 0;
     DevState *ds;
     e = dev_state(dev, &ds);
@@ -1063,7 +1145,17 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
     // one launch per stripe (launch-bound below ~4 MiB of data per stripe)
     if (mode == kModeAuto && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) &&
         code->q * code->t <= size_t(kMaxTn))
-        return encode_staged_batch(cs, *ds, dev, data, par, n_stripes, chunk, st);
+        return encode_staged_batch(cs, *ds, dev, data, par, n_stripes, chunk, st, sd);
+    std::vector<const uint8_t *> dv;
+    std::vector<uint8_t *> pv;
+    if (sd) {  // per-stripe kernels below take pointer arrays
+        for (size_t s = 0; s < n_stripes; s++) {
+            for (size_t i = 0; i < code->k; i++) dv.push_back(sd->data + int64_t(s) * sd->dstripe + int64_t(i) * sd->dnode);
+            for (size_t i = 0; i < code->m; i++) pv.push_back(sd->par + int64_t(s) * sd->pstripe + int64_t(i) * sd->pnode);
+        }
+        data = dv.data();
+        par = pv.data();
+    }
     if (mode == kModeAuto || mode >= kModeBs) {
         bool done = false;
         e = encode_bitsliced(cs, dev, data, par, n_stripes, chunk, st, mode, tile, &done);
@@ -1275,6 +1367,16 @@ int clay_encode_device_batch(const clay_code_t *code, const uint8_t *const *data
                              size_t chunk, int device, void *stream, clay_error_t *err) {
     if (err) std::memset(err, 0, sizeof(*err));
     Error e = encode_device_impl(code, data, par, ns, chunk, device, stream);
+    return e ? report(e, err) : 0;
+}
+
+int clay_encode_device_strided(const clay_code_t *code, const uint8_t *data, int64_t data_node_stride,
+                               int64_t data_stripe_stride, uint8_t *parity, int64_t parity_node_stride,
+                               int64_t parity_stripe_stride, size_t n_stripes, size_t chunk, int device, void *stream,
+                               clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    const Strided sd{data, data_node_stride, data_stripe_stride, parity, parity_node_stride, parity_stripe_stride};
+    Error e = encode_device_impl(code, nullptr, nullptr, n_stripes, chunk, device, stream, &sd);
     return e ? report(e, err) : 0;
 }
 

@@ -157,6 +157,18 @@ int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *da
                                uint8_t *const *parity_chunks, size_t chunk_size, int device,
                                size_t piece_bytes, int n_streams, clay_error_t *err);
 
+/* Batched encode of n_stripes stripes laid out at fixed strides in device memory
+ * (the reference encodes one stripe per call, encode.rs:30-80):
+ * data node i of stripe s at data + s*data_stripe_stride + i*data_node_stride, parity
+ * node j at parity + s*parity_stripe_stride + j*parity_node_stride (bytes; e.g. a
+ * contiguous [n_stripes][k][chunk] buffer has node stride chunk, stripe stride k*chunk).
+ * Same results as clay_encode_device_batch with the equivalent pointer arrays, with O(1)
+ * host work per call.  Asynchronous on `stream`. */
+int clay_encode_device_strided(const clay_code_t *code, const uint8_t *data, int64_t data_node_stride,
+                               int64_t data_stripe_stride, uint8_t *parity, int64_t parity_node_stride,
+                               int64_t parity_stripe_stride, size_t n_stripes, size_t chunk_size, int device,
+                               void *stream, clay_error_t *err);
+
 /* Decode / rebuild on device.  chunks: n device pointers, NULL for every erased
  * node (validation as decode.rs:36-126 with available = the non-NULL entries).
  * out_chunks: n device pointers; for every erased DATA node out_chunks[i] must

@@ -404,7 +404,7 @@ def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg):
 
 
 @pytest.mark.parametrize("cfg", [(4, 2, 5), (10, 4, 13), (9, 3, 11), (6, 3, 8), (5, 3, 6)])
-@pytest.mark.parametrize("sc,n", [(32, 4), (16 * 70 + 6, 9), (4096, 5)])
+@pytest.mark.parametrize("sc,n", [(32, 4), (2, 300), (32, 301), (320, 37), (16 * 70 + 6, 9), (4096, 5), (4104, 6)])
 def test_encode_device_batch_small_stripes(oracle_mod, torch_cuda, cfg, sc, n):
     """Batched small stripes: one launch per plan level for the whole batch (grid.y =
     stripe, device pointer table); every stripe's parity equals the oracle's."""

@@ -192,3 +192,53 @@ def test_batch_encode_more_than_grid_y_limit(oracle_mod, torch_cuda):
     for s in (0, 1, 65534, 65535, 65536, n - 1):
         ref = o.encode_array(host[s * k:(s + 1) * k].reshape(-1))
         assert np.array_equal(got[s * m:(s + 1) * m], ref[k:]), s
+
+
+@pytest.mark.parametrize("sc,n", [(32, 300), (4104, 5)])
+def test_batch_encode_non_affine_pointers(oracle_mod, torch_cuda, sc, n):
+    """Stripes whose chunks are NOT rows of one strided buffer (permuted order) take the
+    device pointer-table path; a second call with the same buffers reuses the cached
+    table.  Affine batches (the other tests) pass base + stride in kernel arguments."""
+    torch = torch_cuda
+    k, m, d = 6, 3, 8
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    chunk = c.sub_chunk_no * sc
+    refs = [_stripe(o, k, chunk, 900 + s) for s in range(n)]
+    perm = np.random.default_rng(3).permutation(n)
+    data = torch.from_numpy(np.concatenate([refs[s][:k] for s in perm])).cuda()
+    par = torch.zeros((n * m, chunk), dtype=torch.uint8, device="cuda")
+    slot = {s: j for j, s in enumerate(perm)}  # stripe s lives at data block slot[s]
+    dl = [data[slot[s] * k + i] for s in range(n) for i in range(k)]
+    pl = [par[slot[s] * m + i] for s in range(n) for i in range(m)]
+    for _ in range(2):
+        par.zero_()
+        c.encode_device_batch(dl, pl, n, chunk)
+        torch.cuda.synchronize()
+        got = par.cpu().numpy()
+        for s in range(n):
+            assert np.array_equal(got[slot[s] * m:(slot[s] + 1) * m], refs[s][k:]), s
+
+
+@pytest.mark.parametrize("cfg,sc,n,pad", [((4, 2, 5), 32, 300, 0), ((4, 2, 5), 32, 3, 0), ((10, 4, 13), 40, 9, 64),
+                                          ((9, 3, 11), 2, 257, 16), ((6, 3, 8), 4104, 5, 0),
+                                          ((10, 4, 13), 2048, 5, 0)])
+def test_encode_device_strided(oracle_mod, torch_cuda, cfg, sc, n, pad):
+    """clay_encode_device_strided: stripes at fixed strides (node stride = chunk + pad),
+    small batches (staged batch), n < 4 and > 4 MiB stripes (per-stripe kernels)."""
+    torch = torch_cuda
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    chunk = c.sub_chunk_no * sc
+    row = chunk + pad
+    refs = [_stripe(o, k, chunk, 1300 + s) for s in range(n)]
+    host = np.zeros((n, k, row), np.uint8)
+    for s in range(n):
+        host[s, :, :chunk] = refs[s][:k]
+    data = torch.from_numpy(host).cuda()
+    par = torch.zeros((n, m, row), dtype=torch.uint8, device="cuda")
+    c.encode_device_strided(data, par, n, chunk, row, k * row, row, m * row)
+    torch.cuda.synchronize()
+    got = par.cpu().numpy()
+    for s in range(n):
+        assert np.array_equal(got[s, :, :chunk], refs[s][k:]), s
+        assert not got[s, :, chunk:].any()
