@@ -120,6 +120,7 @@ if __name__ == "__main__":
     prewarm(float(os.environ.get("PREWARM_MS", "250")))
     encode_cfg(10, 4, 13, 1 << 30)
     encode_cfg(4, 2, 5, 64 << 20)
+    encode_cfg(9, 3, 11, 9 * (256 << 20))
     encode_batch_cfg(4, 2, 5, 1 << 20, 256)
     decode_cfg(4, 2, 5, 64 << 20, [0])
     decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])

@@ -317,14 +317,51 @@ def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda):
 
 
 @pytest.mark.slow
-def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda):
+def test_cfg5_10_4_13_1GiB_decode_4_erasures_codeword_incl_parity(oracle_mod, torch_cuda):
+    """The same 4-erasure pattern on a real 1 GiB codeword (encoded by the oracle): every
+    erased node comes back, the rebuilt parity node 12 (internal 14) included."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    data = rand_bytes(55, 1 << 30)
+    ref = o.encode_array(data)
+    chunk = ref.shape[1]
+    er = [0, 4, 8, 12]
+    full = torch.from_numpy(ref).cuda()
+    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                    [outs[i] if i in er else None for i in range(14)], chunk)
+    torch.cuda.synchronize()
+    for e in er:
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
+
+
+@pytest.mark.slow
+def test_cfg3_9_3_11_encode_full_size(oracle_mod, torch_cuda):
+    """(9,3,11) stripe of 9 x 256 MiB: chunk 268,435,458, sc 3,314,018 (= 2 mod 8, off the
+    bit-sliced kernels' 8-byte gate), whole parity against the oracle."""
+    torch = torch_cuda
+    c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
+    data = rand_bytes(93, 9 * (256 << 20))
+    ref = o.encode_array(data)
+    chunk = ref.shape[1]
+    assert chunk == 268_435_458
+    dev = torch.from_numpy(ref[:9].copy()).cuda()
+    par = torch.zeros((3, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device([dev[i] for i in range(9)], [par[i] for i in range(3)], chunk)
+    torch.cuda.synchronize()
+    assert np.array_equal(par.cpu().numpy(), ref[9:]), clay_amd.last_encode_path()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("lost", [0, 11])
+def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda, lost):
+    """Node 0 (data) and node 11 (last parity, the slowest plan in bench_paths)."""
     torch = torch_cuda
     c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
     chunk = 268_435_458
     sc = chunk // 81
-    rng = np.random.default_rng(8)
-    lost = 0
-    info = c.minimum_to_repair(lost, list(range(1, 12)))
+    rng = np.random.default_rng(8 + lost)
+    info = c.minimum_to_repair(lost, [i for i in range(12) if i != lost])
     assert len(info) == 11 and len(info[0][1]) == 27
     pd = {h: rng.integers(0, 256, 27 * sc, dtype=np.uint8) for h, _ in info}
     ref = np.frombuffer(o.repair(lost, pd, chunk), np.uint8)
