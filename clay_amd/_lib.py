@@ -9,7 +9,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libclay_amd.so")
+# CLAY_AMD_LIB selects another build of the same library (the sanitizer build of
+# scripts/asan_check.sh); it is never a fallback: a missing library still raises.
+LIB_PATH = os.environ.get("CLAY_AMD_LIB") or os.path.join(_HERE, "libclay_amd.so")
 
 CLAY_ERR_DEVICE = 100
 

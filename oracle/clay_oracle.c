@@ -417,6 +417,9 @@ static void u_from_c_and_ustar(const uint8_t *cxy, const uint8_t *uc, uint8_t *u
     uint8_t det = 1 ^ MUL_TABLE[GAMMA][GAMMA];
     for (size_t i = 0; i < len; i++) u[i] = MUL_TABLE[det][cxy[i]] ^ MUL_TABLE[GAMMA][uc[i]];
 }
+/* exported for the reference's test_partial_transform_roundtrips (transforms.rs:192-213) */
+void oc_c_from_u_and_cstar(const uint8_t *u, const uint8_t *cs, uint8_t *c, size_t len) { c_from_u_and_cstar(u, cs, c, len); }
+void oc_u_from_c_and_ustar(const uint8_t *c, const uint8_t *us, uint8_t *u, size_t len) { u_from_c_and_ustar(c, us, u, len); }
 /* decode.rs:566-576 compute_cstar_from_c_and_u */
 static void cstar_from_c_and_u(const uint8_t *ch, const uint8_t *uh, uint8_t *out, size_t len) {
     uint8_t gi = oc_gf_div(1, GAMMA);

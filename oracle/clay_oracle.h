@@ -65,6 +65,9 @@ int oc_repair_subchunk_indices(const oc_code_t *p, size_t lost_internal, size_t 
                                size_t *n_out, oc_error_t *err);
 void oc_prt(const uint8_t *c, const uint8_t *cs, uint8_t *u, uint8_t *us, size_t len);
 void oc_pft(const uint8_t *u, const uint8_t *us, uint8_t *c, uint8_t *cs, size_t len);
+/* transforms.rs:132-142 / 149-161 (partial transforms) */
+void oc_c_from_u_and_cstar(const uint8_t *u, const uint8_t *cs, uint8_t *c, size_t len);
+void oc_u_from_c_and_ustar(const uint8_t *c, const uint8_t *us, uint8_t *u, size_t len);
 
 /* ---- ClayCode API (lib.rs:94-241) ---- */
 int oc_new(size_t k, size_t m, size_t d, oc_code_t *out, oc_error_t *err);

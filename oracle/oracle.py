@@ -18,7 +18,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# CLAY_ORACLE_LIB: the sanitizer build (scripts/asan_check.sh), built by its own make target
+_LIB_PATH = os.environ.get("CLAY_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 
 ERROR_NAMES = {
     1: "InvalidParameters",
@@ -56,6 +57,8 @@ class OracleError(Exception):
 def build() -> str:
     """Compile liboracle.so (gcc) if missing or stale."""
     src = os.path.join(_HERE, "clay_oracle.c")
+    if os.environ.get("CLAY_ORACLE_LIB"):
+        return _LIB_PATH
     if (not os.path.exists(_LIB_PATH)
             or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
         subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -92,6 +95,8 @@ def lib():
         L.oc_repair_subchunk_indices.argtypes = [P(OcCode), sz, P(sz), P(sz), P(OcError)]
         L.oc_prt.argtypes = [u8p, u8p, u8p, u8p, sz]
         L.oc_pft.argtypes = [u8p, u8p, u8p, u8p, sz]
+        L.oc_c_from_u_and_cstar.argtypes = [u8p, u8p, u8p, sz]
+        L.oc_u_from_c_and_ustar.argtypes = [u8p, u8p, u8p, sz]
         L.oc_new.argtypes = [sz, sz, sz, P(OcCode), P(OcError)]
         L.oc_new_default.argtypes = [sz, sz, P(OcCode), P(OcError)]
         L.oc_normalized_repair_bandwidth.restype = C.c_double
@@ -173,6 +178,22 @@ def pft(u, us):
     c, cs = np.zeros_like(u), np.zeros_like(u)
     lib().oc_pft(_u8(u), _u8(us), _u8(c), _u8(cs), u.size)
     return c.tolist(), cs.tolist()
+
+
+def c_from_u_and_cstar(u, cs):
+    """transforms.rs:132-142: C = U + gamma * C*."""
+    u, cs = _as_np(u), _as_np(cs)
+    c = np.zeros_like(u)
+    lib().oc_c_from_u_and_cstar(_u8(u), _u8(cs), _u8(c), u.size)
+    return c.tolist()
+
+
+def u_from_c_and_ustar(c, us):
+    """transforms.rs:149-161: U = det * C + gamma * U*."""
+    c, us = _as_np(c), _as_np(us)
+    u = np.zeros_like(c)
+    lib().oc_u_from_c_and_ustar(_u8(c), _u8(us), _u8(u), c.size)
+    return u.tolist()
 
 
 def set_simd(enable: bool):

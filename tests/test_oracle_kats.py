@@ -73,6 +73,16 @@ def test_transforms_kats(oracle_mod):
     assert O.gf_inv(1 ^ O.gf_mul(2, 2)) == 0xA7 and O.gf_inv(2) == 0x8E
 
 
+def test_partial_transform_roundtrips(oracle_mod):
+    """transforms.rs:192-213: the partial transforms agree with the full PRT / PFT."""
+    O = oracle_mod
+    c, cs = [0x12, 0x34, 0x56, 0x78], [0xAB, 0xCD, 0xEF, 0x01]
+    u, us = O.prt(c, cs)                      # full PRT: (C, C*) -> (U, U*)
+    assert O.c_from_u_and_cstar(u, cs) == c   # given U and C*, recover C
+    assert O.u_from_c_and_ustar(c, us) == u   # given C and U*, recover U
+    assert O.pft(u, us) == (c, cs)            # and the PFT round trip
+
+
 def test_plane_vector_kats(oracle_mod):
     """coords.rs:42-61."""
     pv = oracle_mod.plane_vector
