@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -35,8 +36,11 @@ static float run(BsArgs a, int reps) {
     return t[t.size() / 2];
 }
 
-int main() {
-    const uint32_t sc = 419432;
+int main(int argc, char **argv) {
+    // sc of the BASELINE stripe by default; another value (e.g. 419456 = 128-aligned rows)
+    // isolates the cost of the 8-byte row alignment of the reference layout
+    const uint32_t sc = argc > 1 ? uint32_t(atoi(argv[1])) : 419432;
+    const bool quick = argc > 2;
     const size_t chunk = size_t(sc) * 256;
     uint8_t *data, *par;
     if (hipMalloc(&data, 10 * chunk) != hipSuccess || hipMalloc(&par, 4 * chunk) != hipSuccess) return 1;
@@ -59,6 +63,16 @@ int main() {
     };
     for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
     (void)hipDeviceSynchronize();
+    if (quick) {
+        printf("sc %u\n", sc);
+        for (int rr = 0; rr < 2; rr++) {
+            rep("L4 full", run<4, 0>(a, 15));
+            rep("L4 no math (memory only)", run<4, 1>(a, 15));
+            rep("L4 reads", run<4, 5>(a, 15));
+            rep("L4 stores only", run<4, 3>(a, 15));
+        }
+        return 0;
+    }
     for (int rr = 0; rr < 2; rr++) {
         rep("L0 full", run<0, 0>(a, 15));
         rep("L1 full", run<1, 0>(a, 15));

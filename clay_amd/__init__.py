@@ -274,6 +274,24 @@ class ClayCode:
         if rc:
             _raise(rc, err)
 
+    def chunk_to_ygroup(self, y: int, chunk, group, chunk_size: int, device: int = 0, stream: int = 0):
+        """Reorder a device chunk into the y-grouped layout of y-section y (clay.h)."""
+        err = ClayErrorStruct()
+        rc = _lib.lib().clay_chunk_to_ygroup(C.byref(self._c), int(y), C.c_void_p(_ptr(chunk)),
+                                             C.c_void_p(_ptr(group)), int(chunk_size), int(device),
+                                             C.c_void_p(int(stream)), C.byref(err))
+        if rc:
+            _raise(rc, err)
+
+    def ygroup_to_chunk(self, y: int, group, chunk, chunk_size: int, device: int = 0, stream: int = 0):
+        """Inverse of chunk_to_ygroup."""
+        err = ClayErrorStruct()
+        rc = _lib.lib().clay_ygroup_to_chunk(C.byref(self._c), int(y), C.c_void_p(_ptr(group)),
+                                             C.c_void_p(_ptr(chunk)), int(chunk_size), int(device),
+                                             C.c_void_p(int(stream)), C.byref(err))
+        if rc:
+            _raise(rc, err)
+
     def reserve_workspace(self, chunk_size: int, device: int = 0):
         """Pre-allocate a pooled workspace and upload the encode plan (clay.h)."""
         err = ClayErrorStruct()

@@ -181,6 +181,38 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
 
 
 // ---------------------------------------------------------------------------
+// Y-grouped chunk layout (docs/clay-practical-implementation.md
+// "Option C", written there with least-significant-digit-first layer digits; here the
+// crate's most-significant-digit-first convention, coords.rs:30-40).  For y-section y the
+// chunk's alpha sub-chunks are reordered as q blocks x = 0..q-1 of beta sub-chunks, block x
+// holding the layers z with digit_y(z) == x in ascending z -- exactly the sub-chunks
+// repair of node (y, x) reads from every helper (repair.rs:22-49), so a helper's repair
+// payload is one contiguous range: group + x * beta * sc.
+// ---------------------------------------------------------------------------
+// Layer of position i of group y: insert digit x = i / beta at digit y of p = i % beta.
+__device__ __forceinline__ uint32_t ygroup_layer(uint32_t i, uint32_t beta, uint32_t q, uint32_t pw) {
+    const uint32_t x = i / beta, p = i - x * beta;  // pw = q^(t-1-y)
+    return ((p / pw) * q + x) * pw + p % pw;
+}
+// TO_GROUP: dst position i <- src layer z(i); else dst layer z(i) <- src position i.
+// One block per (sub-chunk, 4 KiB piece); 16-byte lanes at any alignment.
+template <bool TO_GROUP>
+__global__ __launch_bounds__(256) void k_ygroup(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint64_t sc,
+                                                uint32_t beta, uint32_t q, uint32_t pw, uint32_t pieces) {
+    const uint32_t i = blockIdx.x / pieces, piece = blockIdx.x - i * pieces;
+    const uint64_t z = ygroup_layer(i, beta, q, pw);
+    const uint64_t so = (TO_GROUP ? z : i) * sc, dofs = (TO_GROUP ? i : z) * sc;
+    const uint64_t b = (uint64_t(piece) * 256 + threadIdx.x) * 16;
+    if (b + 16 <= sc) {
+        uint4 v;
+        __builtin_memcpy(&v, src + so + b, 16);
+        __builtin_memcpy(dst + dofs + b, &v, 16);
+    } else {
+        for (uint64_t j = b; j < sc; j++) dst[dofs + j] = src[so + j];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Fused encode (parity = last y-section).  See file header and DESIGN.md.
 // LDS: acc[p][z][W] bytes (p < Q parity rows, z < alpha layers, W positions).
 // ---------------------------------------------------------------------------
@@ -1377,6 +1409,50 @@ int clay_encode_device_strided(const clay_code_t *code, const uint8_t *data, int
     if (err) std::memset(err, 0, sizeof(*err));
     const Strided sd{data, data_node_stride, data_stripe_stride, parity, parity_node_stride, parity_stripe_stride};
     Error e = encode_device_impl(code, nullptr, nullptr, n_stripes, chunk, device, stream, &sd);
+    return e ? report(e, err) : 0;
+}
+
+static Error ygroup_impl(const clay_code_t *code, size_t y, const uint8_t *src, uint8_t *dst, size_t chunk, int dev,
+                         void *stream, bool to_group) {
+    Error e = check_code(code);
+    if (e) return e;
+    if (!src || !dst) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null chunk");
+    if (y >= code->t)
+        return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: y-section %zu >= t = %zu", y,
+                          code->t);
+    if (chunk == 0 || chunk % code->sub_chunk_no != 0)
+        return make_error(CLAY_ERR_INVALID_CHUNK_SIZE, code->sub_chunk_no, chunk, 0,
+                          "Invalid chunk size: expected divisible by %zu, got %zu", code->sub_chunk_no, chunk);
+    if (src == dst) return make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: in-place regroup");
+    DevState *ds;
+    e = dev_state(dev, &ds);
+    if (e) return e;
+    DeviceGuard g(dev);
+    const uint64_t sc = chunk / code->sub_chunk_no;
+    size_t pw = 1;
+    for (size_t j = y + 1; j < code->t; j++) pw *= code->q;
+    const uint64_t pieces = (sc + 4095) / 4096;
+    const uint64_t blocks = uint64_t(code->sub_chunk_no) * pieces;
+    if (blocks > 0x7fffffffull) return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "chunk too large for one regroup launch");
+    auto k = to_group ? k_ygroup<true> : k_ygroup<false>;
+    k<<<dim3(uint32_t(blocks)), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
+        src, dst, sc, uint32_t(code->beta), uint32_t(code->q), uint32_t(pw), uint32_t(pieces));
+    CLAY_HIP(hipGetLastError());
+    t_last_launches = 1;
+    return Error{};
+}
+
+int clay_chunk_to_ygroup(const clay_code_t *code, size_t y, const uint8_t *chunk, uint8_t *group, size_t chunk_size,
+                         int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = ygroup_impl(code, y, chunk, group, chunk_size, device, stream, true);
+    return e ? report(e, err) : 0;
+}
+
+int clay_ygroup_to_chunk(const clay_code_t *code, size_t y, const uint8_t *group, uint8_t *chunk, size_t chunk_size,
+                         int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = ygroup_impl(code, y, group, chunk, chunk_size, device, stream, false);
     return e ? report(e, err) : 0;
 }
 

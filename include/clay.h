@@ -169,6 +169,19 @@ int clay_encode_device_strided(const clay_code_t *code, const uint8_t *data, int
                                int64_t parity_stripe_stride, size_t n_stripes, size_t chunk_size, int device,
                                void *stream, clay_error_t *err);
 
+/* Y-grouped chunk layout ("Option C" of the reference's
+ * docs/clay-practical-implementation.md:416-582, in the crate's MSB-first digit order):
+ * for y-section y, the chunk's alpha sub-chunks reordered as blocks x = 0..q-1 of beta
+ * sub-chunks, block x = the layers z with digit_y(z) == x in ascending order
+ * (= get_repair_subchunk_indices of node (y, x), repair.rs:22-49).  A helper stored this
+ * way serves the repair of node (y, x) from ONE contiguous range, group + x*beta*sc, which
+ * can be passed straight to clay_repair_device.  Device buffers of chunk_size bytes, not
+ * in place; asynchronous on `stream`. */
+int clay_chunk_to_ygroup(const clay_code_t *code, size_t y, const uint8_t *chunk, uint8_t *group,
+                         size_t chunk_size, int device, void *stream, clay_error_t *err);
+int clay_ygroup_to_chunk(const clay_code_t *code, size_t y, const uint8_t *group, uint8_t *chunk,
+                         size_t chunk_size, int device, void *stream, clay_error_t *err);
+
 /* Decode / rebuild on device.  chunks: n device pointers, NULL for every erased
  * node (validation as decode.rs:36-126 with available = the non-NULL entries).
  * out_chunks: n device pointers; for every erased DATA node out_chunks[i] must

@@ -263,6 +263,46 @@ def test_device_api_encode_decode_repair(oracle_mod, torch_cuda):
 # ---------------------------------------------------------------------------
 # BASELINE.json configurations at full size
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("size", [1024, 10 * 1024, 100 * 1024, 1 << 20])
+def test_cfg1_4_2_5_clay_bench_sizes(oracle_mod, torch_cuda, size):
+    """BASELINE configs[0] / benches/clay_bench.rs:20-56 shape: (4,2,5) encode of 1 KiB -
+    1 MiB (1 MiB: chunk 262,144, sub-chunk 32,768) through every entry point -- host
+    clay_encode, clay_encode_device (one stripe), clay_encode_device_batch and
+    clay_encode_device_strided (64 stripes) -- plus the bench's decode (1 erasure) and
+    repair legs, all against the oracle."""
+    torch = torch_cuda
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    data = rand_bytes(size, size)
+    ref = o.encode_array(data)
+    chunk = ref.shape[1]
+    if size == 1 << 20:
+        assert chunk == 262_144 and chunk // c.sub_chunk_no == 32_768
+    assert np.array_equal(c.encode_array(data), ref)
+    dev = torch.from_numpy(ref[:4].copy()).cuda()
+    par = torch.zeros((2, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device([dev[i] for i in range(4)], [par[i] for i in range(2)], chunk)
+    torch.cuda.synchronize()
+    assert np.array_equal(par.cpu().numpy(), ref[4:])
+    n = 64
+    refs = [o.encode_array(rand_bytes(size + s, size)) for s in range(n)]
+    bd = torch.from_numpy(np.stack([r[:4] for r in refs])).cuda()
+    bp = torch.zeros((n, 2, chunk), dtype=torch.uint8, device="cuda")
+    c.encode_device_batch([bd[s, i] for s in range(n) for i in range(4)], [bp[s, j] for s in range(n) for j in range(2)],
+                          n, chunk)
+    torch.cuda.synchronize()
+    assert np.array_equal(bp.cpu().numpy(), np.stack([r[4:] for r in refs]))
+    bp.zero_()
+    c.encode_device_strided(bd, bp, n, chunk)
+    torch.cuda.synchronize()
+    assert np.array_equal(bp.cpu().numpy(), np.stack([r[4:] for r in refs]))
+    av = {i: ref[i] for i in range(1, 6)}                       # clay_bench.rs decode leg
+    assert c.decode(av, [0]) == o.decode(av, [0])
+    info = c.minimum_to_repair(0, [1, 2, 3, 4, 5])              # clay_bench.rs repair leg
+    sc = chunk // c.sub_chunk_no
+    pd = {h: np.concatenate([ref[h][z * sc:(z + 1) * sc] for z in idx]) for h, idx in info}
+    assert c.repair(0, pd, chunk) == o.repair(0, pd, chunk) == ref[0].tobytes()
+
+
 @pytest.mark.slow
 def test_cfg2_4_2_5_64MiB_encode_decode(oracle_mod):
     c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)

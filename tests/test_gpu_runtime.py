@@ -242,3 +242,49 @@ def test_encode_device_strided(oracle_mod, torch_cuda, cfg, sc, n, pad):
     for s in range(n):
         assert np.array_equal(got[s, :, :chunk], refs[s][k:]), s
         assert not got[s, :, chunk:].any()
+
+
+# ---------------------------------------------------------------------------
+# Y-grouped ("Option C") layout, SURVEY.md §8f item 3
+# ---------------------------------------------------------------------------
+def ygroup_order(c, y):
+    """docs/clay-practical-implementation.md:453-490 construct_groups, restated with the
+    crate's MSB-first digits (coords.rs:30-40): blocks x of layers with digit_y == x."""
+    q, t, alpha = c.q, c.t, c.sub_chunk_no
+    digit = lambda z: (z // q ** (t - 1 - y)) % q  # noqa: E731
+    return [z for x in range(q) for z in range(alpha) if digit(z) == x]
+
+
+@pytest.mark.parametrize("cfg,sc", [((10, 4, 13), 100), ((9, 3, 11), 4098), ((4, 2, 5), 9000), ((6, 3, 8), 2)])
+def test_ygroup_layout_and_repair(oracle_mod, torch_cuda, cfg, sc):
+    """Regroup = the restated permutation; inverse restores the chunk; repairing node
+    (y, x) from each helper's contiguous block x of group y equals the oracle's repair."""
+    torch = torch_cuda
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    chunk = c.sub_chunk_no * sc
+    ref = _stripe(o, k, chunk, 4242 + sc)
+    full = torch.from_numpy(ref).cuda()
+    for lost in range(c.n):
+        li = lost if lost < k else lost + c.nu
+        y, x = divmod(li, c.q)
+        info = c.minimum_to_repair(lost, [i for i in range(c.n) if i != lost])
+        order = ygroup_order(c, y)
+        beta = c.beta
+        assert order[x * beta:(x + 1) * beta] == list(info[0][1])  # block x = repair indices
+        groups = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
+        for h, _ in info:
+            c.chunk_to_ygroup(y, full[h], groups[h], chunk)
+        torch.cuda.synchronize()
+        for h, _ in info:
+            want = ref[h].reshape(c.sub_chunk_no, sc)[order].reshape(-1)
+            assert np.array_equal(groups[h].cpu().numpy(), want), (lost, h)
+        out = torch.zeros(chunk, dtype=torch.uint8, device="cuda")
+        c.repair_device(lost, [h for h, _ in info], [groups[h][x * beta * sc:(x + 1) * beta * sc] for h, _ in info],
+                        chunk, out)
+        back = torch.zeros(chunk, dtype=torch.uint8, device="cuda")
+        h0 = info[0][0]
+        c.ygroup_to_chunk(y, groups[h0], back, chunk)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref[lost]), lost
+        assert np.array_equal(back.cpu().numpy(), ref[h0])
