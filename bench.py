@@ -40,6 +40,8 @@ sys.path.insert(0, ROOT)
 K, M, D = 10, 4, 13
 STRIPE_BYTES = 1 << 30  # reference ClayCode::encode input
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+# best copy kernel measured on this pool (bench_tools/bw_probe.hip, profiles/r02_probes/bw_probe_r02a.txt)
+COPY_CEILING_GBS = 5418.0
 VERIFY_W = 4096         # positions per verified column slice (every rank, both ends)
 
 
@@ -417,6 +419,8 @@ def run_rank(args) -> int:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "measured_copy_ceiling": COPY_CEILING_GBS,
+                     "frac_of_measured_copy": round(achieved / COPY_CEILING_GBS, 4),
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_ms_mean": round(mean_ms, 4), "kernel_ms_min": round(min(kern_ms), 4)},
         "verified_vs_oracle": verified if world == 1 else all(bool(p[2]) for p in per),
