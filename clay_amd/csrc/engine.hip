@@ -23,6 +23,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -446,11 +447,7 @@ struct DevState {
     std::vector<std::unique_ptr<Lease>> pool;    // workspaces and staging buffers
     std::map<std::vector<uint8_t *>, PtrTable> tables;
     uint64_t tick = 0;
-    std::vector<hipStream_t> host_streams;       // idle streams of the host-buffer API
-    // host-streaming pipeline (clay_encode_host_pipelined): streams + per-stream piece buffers
-    std::mutex pipe_mu;
-    std::vector<hipStream_t> pipe_streams;
-    std::vector<Lease> pipe_bufs;
+    std::vector<hipStream_t> host_streams;       // idle streams of the host-streaming pipeline
 };
 static DevState g_dev[64];
 
@@ -1294,37 +1291,163 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
 }
 
 // ---------------------------------------------------------------------------
-// Host-buffer API helpers: each call takes an idle stream of the current device
-// (created on demand) and pooled staging buffers, so host calls from different
-// threads run concurrently.
-// ---------------------------------------------------------------------------
-struct HostCall {
-    int dev = 0;
-    DevState *ds = nullptr;
-    hipStream_t st = nullptr;
-    ~HostCall() {
-        if (ds && st) {
-            std::lock_guard<std::mutex> lk(ds->mu);
-            ds->host_streams.push_back(st);
-        }
-    }
-    Error begin() {
-        int ndev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-            return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: no GPU device available (no CPU fallback)");
-        (void)hipGetDevice(&dev);
-        Error e = dev_state(dev, &ds);
-        if (e) return e;
-        std::lock_guard<std::mutex> lk(ds->mu);
-        if (!ds->host_streams.empty()) {
-            st = ds->host_streams.back();
-            ds->host_streams.pop_back();
-        } else {
-            CLAY_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-        }
-        return Error{};
-    }
+// Host-side copies the API's semantics require (the returned data chunks, encode.rs:44-55 /
+// decode.rs:155-158), split over a few threads and run beside the GPU pipeline.
+struct CopyJob {
+    uint8_t *dst;
+    const uint8_t *src;  // nullptr: zero fill
+    size_t n;
 };
+class HostCopier {
+  public:
+    explicit HostCopier(std::vector<CopyJob> jobs) : jobs_(std::move(jobs)) {
+        size_t total = 0;
+        for (auto &j : jobs_) total += j.n;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const size_t nt = std::min<size_t>({8, hw, std::max<size_t>(1, total >> 24)});  // >= 16 MiB per thread
+        const size_t per = (total + nt - 1) / std::max<size_t>(1, nt);
+        for (size_t t = 0; t < nt && total; t++)
+            th_.emplace_back([this, t, per] { run(t * per, (t + 1) * per); });
+    }
+    ~HostCopier() { join(); }
+    void join() {
+        for (auto &t : th_)
+            if (t.joinable()) t.join();
+    }
+
+  private:
+    void run(size_t lo, size_t hi) {  // byte range [lo, hi) of the concatenated jobs
+        size_t at = 0;
+        for (auto &j : jobs_) {
+            const size_t a = std::max(lo, at), b = std::min(hi, at + j.n);
+            if (a < b) {
+                if (j.src) std::memcpy(j.dst + (a - at), j.src + (a - at), b - a);
+                else std::memset(j.dst + (a - at), 0, b - a);
+            }
+            at += j.n;
+        }
+    }
+    std::vector<CopyJob> jobs_;
+    std::vector<std::thread> th_;
+};
+
+// Host-streaming pipeline.  Each byte offset of the sub-chunks
+// is an independent codeword, so an operation on host chunks is cut into pieces of `w`
+// bytes of every sub-chunk row.  Piece p of a host buffer of R rows (pitch sc) is one
+// hipMemcpy2DAsync into a compact device buffer (R rows of wp bytes); the device
+// operation runs on the pieces; outputs go back by 2D copies.  Pieces round-robin over
+// the device's pipeline streams, so the H2D of piece p+1, the kernels of piece p and the
+// D2H of piece p-1 overlap (PCIe is full duplex).  Used by clay_encode_host_pipelined and
+// by the host-buffer API (clay_encode / clay_decode / clay_repair).
+struct HostIn {
+    const uint8_t *p;
+    size_t rows;
+};
+struct HostOut {
+    uint8_t *p;
+    size_t rows;
+};
+template <class Op>
+static Error host_pipeline(int device, size_t sc, const std::vector<HostIn> &ins, const std::vector<HostOut> &outs,
+                           size_t piece_bytes, int n_streams, Op &&op, size_t *launches_out) {
+    size_t in_rows = 0, all_rows = 0;
+    for (auto &i : ins) in_rows += i.rows;
+    all_rows = in_rows;
+    for (auto &o : outs) all_rows += o.rows;
+    if (sc == 0 || all_rows == 0) return Error{};
+    // default: 128 MiB of input per piece over 2 streams (sweep: r01 host pipeline), whole
+    // 256-byte tiles; CLAY_HOST_PIECE_MB / CLAY_HOST_STREAMS override the defaults
+    static const size_t def_piece = [] {
+        const char *e = getenv("CLAY_HOST_PIECE_MB");
+        return (e ? size_t(atoi(e)) : size_t(128)) << 20;
+    }();
+    static const int def_streams = [] {
+        const char *e = getenv("CLAY_HOST_STREAMS");
+        return e ? atoi(e) : 2;
+    }();
+    if (n_streams <= 0) n_streams = def_streams;
+    size_t w = piece_bytes ? piece_bytes : def_piece / std::max<size_t>(1, in_rows);
+    w = w >= 256 ? w / 256 * 256 : (w + 7) / 8 * 8;
+    w = std::max<size_t>(8, std::min(w, sc));
+    const size_t np = (sc + w - 1) / w;
+    const int ns = int(std::max<size_t>(1, std::min<size_t>(np, n_streams > 0 ? size_t(n_streams) : 2)));
+    DevState *ds;
+    Error e = dev_state(device, &ds);
+    if (e) return e;
+    DeviceGuard g(device);
+    // streams and piece buffers of this call: from the device's pools (no device-wide
+    // lock across the call, so pipelined calls from several threads run concurrently)
+    struct Res {
+        DevState &ds;
+        std::vector<hipStream_t> st;
+        std::vector<Lease *> buf;
+        ~Res() {
+            for (size_t i = 0; i < buf.size(); i++) lease_release(ds, buf[i], st[i]);
+            std::lock_guard<std::mutex> lk(ds.mu);
+            for (auto x : st) ds.host_streams.push_back(x);
+        }
+    } r{*ds, {}, {}};
+    {
+        std::lock_guard<std::mutex> lk(ds->mu);
+        while (int(r.st.size()) < ns) {
+            hipStream_t st;
+            if (!ds->host_streams.empty()) {
+                st = ds->host_streams.back();
+                ds->host_streams.pop_back();
+            } else {
+                CLAY_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            }
+            r.st.push_back(st);
+        }
+    }
+    const size_t need = all_rows * w;
+    for (int s = 0; s < ns; s++) {
+        Lease *l = nullptr;
+        e = lease_acquire(*ds, need, r.st[s], &l);
+        if (e) return e;
+        r.buf.push_back(l);
+    }
+    std::vector<const uint8_t *> din(ins.size());
+    std::vector<uint8_t *> dout(outs.size());
+    size_t launches = 0;
+    for (size_t p = 0; p < np; p++) {
+        const int s = int(p % size_t(ns));
+        hipStream_t st = r.st[s];
+        uint8_t *buf = static_cast<uint8_t *>(r.buf[s]->d);
+        const size_t off = p * w, wp = std::min(w, sc - off);
+        size_t at = 0;
+        for (size_t i = 0; i < ins.size(); i++) {
+            uint8_t *dst = buf + at * wp;
+            if (ins[i].p)
+                CLAY_HIP(hipMemcpy2DAsync(dst, wp, ins[i].p + off, sc, wp, ins[i].rows, hipMemcpyHostToDevice, st));
+            din[i] = ins[i].p ? dst : nullptr;
+            at += ins[i].rows;
+        }
+        for (size_t j = 0; j < outs.size(); j++) {
+            dout[j] = outs[j].p ? buf + at * wp : nullptr;
+            at += outs[j].rows;
+        }
+        e = op(din, dout, wp, st);
+        if (e) return e;
+        launches += t_last_launches;
+        for (size_t j = 0; j < outs.size(); j++)
+            if (outs[j].p)
+                CLAY_HIP(hipMemcpy2DAsync(outs[j].p + off, sc, dout[j], wp, wp, outs[j].rows, hipMemcpyDeviceToHost, st));
+    }
+    for (int s = 0; s < ns; s++) CLAY_HIP(hipStreamSynchronize(r.st[s]));
+    if (launches_out) *launches_out = launches;
+    return Error{};
+}
+
+static int current_device(Error *e) {
+    int ndev = 0, d = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        *e = make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: no GPU device available (no CPU fallback)");
+        return -1;
+    }
+    (void)hipGetDevice(&d);
+    return d;
+}
 
 }  // namespace clay
 
@@ -1595,14 +1718,6 @@ int clay_plan_export(const clay_code_t *code, int kind, const uint8_t *mask, con
     return 0;
 }
 
-// Host-streaming encode.  Each byte offset of the sub-chunks
-// is an independent codeword, so the stripe is cut into pieces of `w` bytes of
-// every sub-chunk.  Piece p of node i is alpha rows of w bytes at pitch sc in
-// host memory -> one hipMemcpy2DAsync into a compact piece buffer (sub-chunk
-// size w), one device encode of that piece, and one 2D copy of each parity piece
-// back.  Pieces round-robin over `ns` streams, so H2D of piece p+1, the encode of
-// piece p and the D2H of piece p-1 overlap (PCIe is full duplex).
-
 int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *data_chunks,
                                uint8_t *const *parity_chunks, size_t chunk, int device, size_t piece_bytes,
                                int n_streams, clay_error_t *err) {
@@ -1620,67 +1735,19 @@ int clay_encode_host_pipelined(const clay_code_t *code, const uint8_t *const *da
         if (!data_chunks[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null data chunk"), err);
     for (size_t i = 0; i < c.m; i++)
         if (!parity_chunks[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null parity chunk"), err);
-    const size_t alpha = c.sub_chunk_no, sc = chunk / alpha, K = c.k, M = c.m;
-    size_t w = piece_bytes ? piece_bytes : (size_t(128) << 20) / (K * alpha);  // sweep: r01 host pipeline
-    w = w >= 256 ? w / 256 * 256 : (w + 7) / 8 * 8;  // whole 256-byte encode tiles (8-byte minimum)
-    w = std::max<size_t>(8, std::min(w, sc));
-    const size_t np = (sc + w - 1) / w;
-    const int ns = int(std::max<size_t>(1, std::min<size_t>(np, n_streams > 0 ? size_t(n_streams) : 2)));
-    DevState *ds;
-    e = dev_state(device, &ds);
-    if (e) return report(e, err);
-    std::lock_guard<std::mutex> pl(ds->pipe_mu);
-    DeviceGuard g(device);
-    auto fail = [&](hipError_t he) {
-        return report(make_error(CLAY_ERR_DEVICE, size_t(he), 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
-    };
-    hipError_t he;
-    while (int(ds->pipe_streams.size()) < ns) {
-        hipStream_t st;
-        if ((he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return fail(he);
-        ds->pipe_streams.push_back(st);
-        ds->pipe_bufs.emplace_back();
-    }
-    const size_t need = (K + M) * alpha * w;
-    for (int s = 0; s < ns; s++) {
-        Lease &b = ds->pipe_bufs[s];
-        if (b.bytes < need) {
-            if (b.d) {
-                if ((he = hipStreamSynchronize(ds->pipe_streams[s])) != hipSuccess) return fail(he);
-                if ((he = hipFree(b.d)) != hipSuccess) return fail(he);
-                b.d = nullptr;
-                b.bytes = 0;
-            }
-            if ((he = hipMalloc(&b.d, need)) != hipSuccess) return fail(he);
-            b.bytes = need;
-        }
-    }
-    std::vector<const uint8_t *> dp(K);
-    std::vector<uint8_t *> pp(M);
+    const size_t alpha = c.sub_chunk_no, sc = chunk / alpha;
+    std::vector<HostIn> ins;
+    std::vector<HostOut> outs;
+    for (size_t i = 0; i < c.k; i++) ins.push_back({data_chunks[i], alpha});
+    for (size_t j = 0; j < c.m; j++) outs.push_back({parity_chunks[j], alpha});
     size_t launches = 0;
-    for (size_t p = 0; p < np; p++) {
-        const int s = int(p % size_t(ns));
-        hipStream_t st = ds->pipe_streams[s];
-        uint8_t *buf = static_cast<uint8_t *>(ds->pipe_bufs[s].d);
-        const size_t off = p * w, wp = std::min(w, sc - off);
-        for (size_t i = 0; i < K; i++) {
-            uint8_t *dst = buf + i * alpha * wp;
-            if ((he = hipMemcpy2DAsync(dst, wp, data_chunks[i] + off, sc, wp, alpha, hipMemcpyHostToDevice, st)) !=
-                hipSuccess)
-                return fail(he);
-            dp[i] = dst;
-        }
-        for (size_t j = 0; j < M; j++) pp[j] = buf + (K + j) * alpha * wp;
-        e = encode_device_impl(code, dp.data(), pp.data(), 1, alpha * wp, device, st);
-        if (e) return report(e, err);
-        launches += t_last_launches;
-        for (size_t j = 0; j < M; j++)
-            if ((he = hipMemcpy2DAsync(parity_chunks[j] + off, sc, pp[j], wp, wp, alpha, hipMemcpyDeviceToHost, st)) !=
-                hipSuccess)
-                return fail(he);
-    }
-    for (int s = 0; s < ns; s++)
-        if ((he = hipStreamSynchronize(ds->pipe_streams[s])) != hipSuccess) return fail(he);
+    e = host_pipeline(device, sc, ins, outs, piece_bytes, n_streams,
+                      [&](const std::vector<const uint8_t *> &din, const std::vector<uint8_t *> &dout, size_t wp,
+                          hipStream_t st) {
+                          return encode_device_impl(code, din.data(), dout.data(), 1, alpha * wp, device, st);
+                      },
+                      &launches);
+    if (e) return report(e, err);
     t_last_launches = launches;
     return 0;
 }
@@ -1700,35 +1767,39 @@ int clay_encode(const clay_code_t *code, const uint8_t *data, size_t len, uint8_
                       err);
     for (size_t i = 0; i < c.n; i++)
         if (!out[i]) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output chunk"), err);
-    // data chunks: zero-padded copy of the input (encode.rs:44-55)
-    for (size_t i = 0; i < c.k; i++) {
-        size_t lo = i * chunk, n = lo < len ? std::min(chunk, len - lo) : 0;
-        if (n) std::memcpy(out[i], data + lo, n);
-        if (n < chunk) std::memset(out[i] + n, 0, chunk - n);
-    }
-    HostCall hc;
-    if ((e = hc.begin())) return report(e, err);
-    const int dev = hc.dev;
-    hipStream_t st = hc.st;
-    LeaseGuard lin(*hc.ds, st), lout(*hc.ds, st);
-    if ((e = lease_acquire(*hc.ds, c.k * chunk, st, &lin.l)) || (e = lease_acquire(*hc.ds, c.m * chunk, st, &lout.l)))
-        return report(e, err);
-    uint8_t *d_data = lin.ptr(), *d_par = lout.ptr();
-    auto fail = [&](hipError_t he) {
-        return report(make_error(CLAY_ERR_DEVICE, size_t(he), 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
-    };
-    hipError_t he;
-    if (len && (he = hipMemcpyAsync(d_data, data, len, hipMemcpyHostToDevice, st)) != hipSuccess) return fail(he);
-    if (c.k * chunk > len && (he = hipMemsetAsync(d_data + len, 0, c.k * chunk - len, st)) != hipSuccess) return fail(he);
-    std::vector<const uint8_t *> dp(c.k);
-    std::vector<uint8_t *> pp(c.m);
-    for (size_t i = 0; i < c.k; i++) dp[i] = d_data + i * chunk;
-    for (size_t i = 0; i < c.m; i++) pp[i] = d_par + i * chunk;
-    e = encode_device_impl(code, dp.data(), pp.data(), 1, chunk, dev, st);
+    const int dev = current_device(&e);
     if (e) return report(e, err);
-    for (size_t i = 0; i < c.m; i++)
-        if ((he = hipMemcpyAsync(out[c.k + i], pp[i], chunk, hipMemcpyDeviceToHost, st)) != hipSuccess) return fail(he);
-    if ((he = hipStreamSynchronize(st)) != hipSuccess) return fail(he);
+    // data chunks: zero-padded copy of the input (encode.rs:44-55).  Chunks wholly inside
+    // the input feed the GPU straight from `data` while host threads copy them into
+    // out[i]; a chunk that needs padding is built first and fed from out[i].
+    const size_t alpha = c.sub_chunk_no, sc = chunk / alpha;
+    std::vector<HostIn> ins;
+    std::vector<CopyJob> jobs;
+    for (size_t i = 0; i < c.k; i++) {
+        const size_t lo = i * chunk, n = lo < len ? std::min(chunk, len - lo) : 0;
+        if (n == chunk) {
+            jobs.push_back({out[i], data + lo, chunk});
+            ins.push_back({data + lo, alpha});
+        } else {
+            if (n) std::memcpy(out[i], data + lo, n);
+            std::memset(out[i] + n, 0, chunk - n);
+            ins.push_back({out[i], alpha});
+        }
+    }
+    HostCopier copier(std::move(jobs));
+    // parity: the host-streaming pipeline
+    std::vector<HostOut> outs;
+    for (size_t j = 0; j < c.m; j++) outs.push_back({out[c.k + j], alpha});
+    size_t launches = 0;
+    e = host_pipeline(dev, sc, ins, outs, 0, 0,
+                      [&](const std::vector<const uint8_t *> &din, const std::vector<uint8_t *> &dout, size_t wp,
+                          hipStream_t st) {
+                          return encode_device_impl(code, din.data(), dout.data(), 1, alpha * wp, dev, st);
+                      },
+                      &launches);
+    copier.join();
+    if (e) return report(e, err);
+    t_last_launches = launches;
     return 0;
 }
 
@@ -1750,38 +1821,33 @@ int clay_decode(const clay_code_t *code, const size_t *ids, const uint8_t *const
         return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: output buffer too small"), err);
     std::vector<const uint8_t *> host_of(c.n, nullptr);
     for (size_t i = 0; i < n_avail; i++) host_of[ids[i]] = bufs[i];
+    std::vector<CopyJob> jobs;  // available data chunks into the output, beside the GPU work
     for (size_t i = 0; i < c.k; i++)
-        if (host_of[i]) std::memcpy(out + i * chunk, host_of[i], chunk);
+        if (host_of[i]) jobs.push_back({out + i * chunk, host_of[i], chunk});
+    HostCopier copier(std::move(jobs));
     bool any_data_erased = false;
     for (size_t i = 0; i < ner; i++) any_data_erased |= er[i] < c.k;
     if (any_data_erased) {
-        HostCall hc;
-        if ((e = hc.begin())) return report(e, err);
-        const int dev = hc.dev;
-        hipStream_t st = hc.st;
-        LeaseGuard lin(*hc.ds, st), lout(*hc.ds, st);
-        if ((e = lease_acquire(*hc.ds, n_avail * chunk, st, &lin.l)) || (e = lease_acquire(*hc.ds, c.k * chunk, st, &lout.l)))
-            return report(e, err);
-        uint8_t *d_in = lin.ptr(), *d_out = lout.ptr();
-        std::vector<const uint8_t *> dch(c.n, nullptr);
-        std::vector<uint8_t *> douts(c.n, nullptr);
-        hipError_t he;
-        for (size_t i = 0; i < n_avail; i++) {
-            he = hipMemcpyAsync(d_in + i * chunk, bufs[i], chunk, hipMemcpyHostToDevice, st);
-            if (he != hipSuccess) return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
-            dch[ids[i]] = d_in + i * chunk;
-        }
-        for (size_t i = 0; i < ner; i++)
-            if (er[i] < c.k) douts[er[i]] = d_out + er[i] * chunk;
-        e = decode_device_impl(code, dch.data(), er, ner, douts.data(), chunk, dev, st);
+        const int dev = current_device(&e);
         if (e) return report(e, err);
+        // pieces of every sub-chunk row: inputs = the available chunks (in internal-node
+        // order), outputs = the erased data chunks straight into `out`
+        const size_t alpha = c.sub_chunk_no, sc = chunk / alpha;
+        std::vector<HostIn> ins(c.n, HostIn{nullptr, alpha});
+        std::vector<HostOut> outs(c.n, HostOut{nullptr, alpha});
+        for (size_t i = 0; i < n_avail; i++) ins[ids[i]].p = bufs[i];
         for (size_t i = 0; i < ner; i++)
-            if (er[i] < c.k) {
-                he = hipMemcpyAsync(out + er[i] * chunk, douts[er[i]], chunk, hipMemcpyDeviceToHost, st);
-                if (he != hipSuccess) return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
-            }
-        he = hipStreamSynchronize(st);
-        if (he != hipSuccess) return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+            if (er[i] < c.k) outs[er[i]].p = out + er[i] * chunk;
+        // the device decode sees chunks[] with nullptr = absent, outs[] for erased data nodes
+        size_t launches = 0;
+        e = host_pipeline(dev, sc, ins, outs, 0, 0,
+                          [&](const std::vector<const uint8_t *> &din, const std::vector<uint8_t *> &dout, size_t wp,
+                              hipStream_t st) {
+                              return decode_device_impl(code, din.data(), er, ner, dout.data(), alpha * wp, dev, st);
+                          },
+                          &launches);
+        if (e) return report(e, err);
+        t_last_launches = launches;
     }
     if (out_len) *out_len = need;
     return 0;
@@ -1801,27 +1867,26 @@ int clay_repair(const clay_code_t *code, size_t lost, const size_t *ids, const u
         if (e) return report(e, err);
     }
     if (!out) return report(make_error(CLAY_ERR_INVALID_PARAMETERS, 0, 0, 0, "Invalid parameters: null output"), err);
-    HostCall hc;
-    if ((e = hc.begin())) return report(e, err);
-    const int dev = hc.dev;
-    hipStream_t st = hc.st;
-    const size_t hb = lens[0];
-    LeaseGuard lin(*hc.ds, st), lout(*hc.ds, st);
-    if ((e = lease_acquire(*hc.ds, nh * hb, st, &lin.l)) || (e = lease_acquire(*hc.ds, chunk, st, &lout.l)))
-        return report(e, err);
-    uint8_t *d_in = lin.ptr(), *d_out = lout.ptr();
-    std::vector<const uint8_t *> dh(nh);
-    hipError_t he;
-    for (size_t i = 0; i < nh; i++) {
-        dh[i] = d_in + i * hb;
-        if (hb && (he = hipMemcpyAsync(d_in + i * hb, bufs[i], hb, hipMemcpyHostToDevice, st)) != hipSuccess)
-            return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
-    }
-    e = repair_device_impl(code, lost, ids, dh.data(), lens, nh, chunk, d_out, dev, st);
+    const int dev = current_device(&e);
     if (e) return report(e, err);
-    if ((he = hipMemcpyAsync(out, d_out, chunk, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (he = hipStreamSynchronize(st)) != hipSuccess)
-        return report(make_error(CLAY_ERR_DEVICE, he, 0, 0, "HIP error: %s", hipGetErrorString(he)), err);
+    // pieces of every sub-chunk row: each helper holds beta rows (its repair layers, in
+    // index order), the output alpha rows
+    const size_t alpha = c.sub_chunk_no, sc = chunk / alpha, beta = nh ? lens[0] / sc : 0;
+    std::vector<HostIn> ins;
+    for (size_t i = 0; i < nh; i++) ins.push_back({bufs[i], beta});
+    std::vector<HostOut> outs{{out, alpha}};
+    std::vector<size_t> plens(nh);
+    size_t launches = 0;
+    e = host_pipeline(dev, sc, ins, outs, 0, 0,
+                      [&](const std::vector<const uint8_t *> &din, const std::vector<uint8_t *> &dout, size_t wp,
+                          hipStream_t st) {
+                          for (auto &l : plens) l = beta * wp;
+                          return repair_device_impl(code, lost, ids, din.data(), plens.data(), nh, alpha * wp, dout[0],
+                                                    dev, st);
+                      },
+                      &launches);
+    if (e) return report(e, err);
+    t_last_launches = launches;
     return 0;
 }
 

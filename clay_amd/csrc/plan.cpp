@@ -2,6 +2,7 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <string>
@@ -256,6 +257,20 @@ void Plan::group_ops() {
             std::vector<uint32_t> cf;
             for (auto &x : t) cf.push_back(x.second);
             gs[gi].coef.push_back(cf);
+        }
+        static const bool dbg = getenv("CLAY_PLAN_DEBUG") != nullptr;
+        if (dbg) {
+            size_t nsrc = 0, ndst = 0;
+            std::map<size_t, size_t> hist;
+            for (auto &g : gs) {
+                nsrc += g.src.size();
+                ndst += g.dst.size();
+                hist[g.dst.size()]++;
+            }
+            fprintf(stderr, "stage %zu: groups %zu src reads %zu dst writes %zu | dst-count histogram:", s, gs.size(), nsrc,
+                    ndst);
+            for (auto &h : hist) fprintf(stderr, " %zu:%zu", h.first, h.second);
+            fprintf(stderr, "\n");
         }
         uint32_t maxd = 1;
         for (auto &g : gs) {
