@@ -1355,11 +1355,11 @@ static Error host_pipeline(int device, size_t sc, const std::vector<HostIn> &ins
     all_rows = in_rows;
     for (auto &o : outs) all_rows += o.rows;
     if (sc == 0 || all_rows == 0) return Error{};
-    // default: 128 MiB of input per piece over 2 streams (sweep: r01 host pipeline), whole
+    // default: 256 MiB of input per piece over 2 streams (scripts/sweep_host_api.sh), whole
     // 256-byte tiles; CLAY_HOST_PIECE_MB / CLAY_HOST_STREAMS override the defaults
     static const size_t def_piece = [] {
         const char *e = getenv("CLAY_HOST_PIECE_MB");
-        return (e ? size_t(atoi(e)) : size_t(128)) << 20;
+        return (e ? size_t(atoi(e)) : size_t(256)) << 20;
     }();
     static const int def_streams = [] {
         const char *e = getenv("CLAY_HOST_STREAMS");
