@@ -108,6 +108,19 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
+_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2}
+
+
+def set_exec_mode(mode: str) -> str:
+    """Process-wide plan executor for decode / repair / staged encode: 'auto' (tile-fused
+    where the U slots fit in LDS, else grouped), 'grouped' (one launch per level) or
+    'tile'.  Every mode produces the reference's bytes.  Returns the previous mode."""
+    if mode not in _EXEC_MODES:
+        raise ValueError(f"unknown exec mode {mode!r}")
+    prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])
+    return {v: k for k, v in _EXEC_MODES.items()}[prev]
+
+
 def release_workspace(device: int = 0) -> None:
     """Free the device's idle pooled buffers and batch pointer tables (clay.h)."""
     err = ClayErrorStruct()

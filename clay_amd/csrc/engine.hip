@@ -182,6 +182,131 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
 
 
 // ---------------------------------------------------------------------------
+// Tile-fused executor (k_texec): ONE launch runs every level of a plan.  A workgroup owns
+// the byte tile [64*VW*blockIdx.x, +64*VW) of every sub-chunk and keeps the plan's U
+// workspace slots for that tile in LDS (dense slot u at u * 64 * VW), so U values never
+// round-trip through HBM and the chip never idles at level boundaries (a level boundary
+// is a workgroup barrier, not a kernel boundary).  Each wave walks its share of a level's
+// groups as a flat stream of (group, source) terms, TEX_BATCH loads in flight at a time
+// across group boundaries -- so 1-2 source groups (repair's C outputs, decode's PFT ops)
+// are not latency-bound -- multiplies every loaded source into up to MAXD destination
+// accumulators, and writes a group's destinations (LDS slot or HBM) after its last term.
+// Eligible when the plan's dense U slot count fits the LDS budget (host: texec_vw).
+// ---------------------------------------------------------------------------
+constexpr int kTexMaxStages = 64;
+constexpr int kTexBatch = 8;
+constexpr size_t kTexLdsMax = 160 * 1024;
+constexpr size_t kTexTabBytes = 256 * 8 * 4;  // perm tables of all GF(2^8) constants
+constexpr size_t kTexAutoGroups = 32;
+
+// Host-flattened term stream (texec_flatten): per level and wave, the terms of the wave's
+// groups back to back, so a batch of term records is one run of independent scalar
+// loads (no group-header -> source-descriptor -> address chain).
+//   x: source base << 24 | slot (U sources: LDS slot)
+//   y, w: the coefficients of destinations 0-3 (y) and 4-7 (w), one byte each
+//   z: ndst << 24, | bit 31 + first destination index on the last term of a group
+// The perm tables of all 256 GF(2^8) constants sit in LDS (8 KiB, behind the U slots), so a
+// multiply's table is a broadcast LDS read instead of a dependent scalar-cache load.
+template <int VW, int MAXD, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_texec(ExecPtrs P, const uint4 *__restrict__ terms,
+                                                    const uint32_t *__restrict__ wbeg,
+                                                    const uint32_t *__restrict__ tabs,
+                                                    const DevSrc *__restrict__ tdsts, uint32_t nstages, uint64_t sc,
+                                                    uint32_t ubase, uint32_t nu) {
+    constexpr int NW = VW / 4;
+    constexpr uint32_t W = 64u * VW;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint64_t pos = uint64_t(blockIdx.x) * W + lane * VW;
+    const bool full = pos + VW <= sc;
+    const uint32_t nb = pos >= sc ? 0u : (full ? uint32_t(VW) : uint32_t(sc - pos));
+    uint8_t *const lds_lane = smem + lane * VW;
+    uint32_t *const ltab = reinterpret_cast<uint32_t *>(smem + size_t(nu) * W);
+    for (uint32_t i = threadIdx.x; i < 256u * 8u; i += 64u * NWV) ltab[i] = tabs[i];
+    __syncthreads();
+    for (uint32_t L = 0; L < nstages; L++) {
+        const uint32_t te = wbeg[L * NWV + wave + 1];
+        uint32_t acc[MAXD][NW];
+#pragma unroll
+        for (int d = 0; d < MAXD; d++)
+#pragma unroll
+            for (int w = 0; w < NW; w++) acc[d][w] = 0;
+        for (uint32_t t = wbeg[L * NWV + wave]; t < te; t += kTexBatch) {
+            uint4 rec[kTexBatch];
+            Words<NW> v[kTexBatch];
+#pragma unroll
+            for (int b = 0; b < kTexBatch; b++) rec[b] = t + b < te ? terms[t + b] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int b = 0; b < kTexBatch; b++) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) v[b].w[w] = 0;
+                if (t + b >= te) continue;
+                const uint32_t base = rec[b].x >> 24, slot = rec[b].x & 0xFFFFFFu;
+                if (base == ubase) {
+                    __builtin_memcpy(&v[b], lds_lane + slot * W, sizeof(v[b]));
+                } else {
+                    const uint8_t *sp = P.p[base] + uint64_t(slot) * sc + pos;
+                    if (full) {
+                        __builtin_memcpy(&v[b], sp, sizeof(v[b]));
+                    } else {
+                        uint8_t tb[VW] = {};
+                        for (uint32_t i = 0; i < nb; i++) tb[i] = sp[i];
+                        __builtin_memcpy(&v[b], tb, sizeof(v[b]));
+                    }
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kTexBatch; b++) {
+                if (t + b >= te) break;
+                const uint32_t nd = (rec[b].z >> 24) & 15u;
+                GfIdx ix[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) ix[w] = gf_idx(v[b].w[w]);
+#pragma unroll
+                for (int d = 0; d < MAXD; d++) {
+                    if (d >= int(nd)) break;
+                    const uint32_t c = ((d < 4 ? rec[b].y : rec[b].w) >> (8 * (d & 3))) & 0xFFu;
+                    if (c == 1u) {
+#pragma unroll
+                        for (int w = 0; w < NW; w++) acc[d][w] ^= v[b].w[w];
+                    } else {
+                        const uint4 t4 = *reinterpret_cast<const uint4 *>(ltab + c * 8u);
+                        const GfTab tab{t4.x, t4.y, t4.z, t4.w, ltab[c * 8u + 4u]};
+#pragma unroll
+                        for (int w = 0; w < NW; w++) acc[d][w] ^= gf_mul_idx(ix[w], tab);
+                    }
+                }
+                if (rec[b].z >> 31) {
+                    const uint32_t db = rec[b].z & 0xFFFFFFu;
+#pragma unroll
+                    for (int d = 0; d < MAXD; d++) {
+                        if (d >= int(nd)) break;
+                        const DevSrc dst = tdsts[db + d];
+                        if (dst.base == ubase) {
+                            __builtin_memcpy(lds_lane + dst.slot * W, acc[d], sizeof(acc[d]));
+                        } else if (nb) {
+                            uint8_t *dp = P.p[dst.base] + uint64_t(dst.slot) * sc + pos;
+                            if (full) {
+                                __builtin_memcpy(dp, acc[d], sizeof(acc[d]));
+                            } else {
+                                uint8_t tb[VW];
+                                __builtin_memcpy(tb, acc[d], sizeof(tb));
+                                for (uint32_t i = 0; i < nb; i++) dp[i] = tb[i];
+                            }
+                        }
+#pragma unroll
+                        for (int w = 0; w < NW; w++) acc[d][w] = 0;
+                    }
+                }
+            }
+        }
+        // level boundary: U slots written above are read by the next level; outputs
+        // written to HBM by this workgroup are visible to it (workgroup-scope fence)
+        if (L + 1 < nstages) __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Y-grouped chunk layout (docs/clay-practical-implementation.md
 // "Option C", written there with least-significant-digit-first layer digits; here the
 // crate's most-significant-digit-first convention, coords.rs:30-40).  For y-section y the
@@ -461,6 +586,12 @@ struct CodeState {
         const DevGroup *groups;
         const DevSrc *srcs, *dsts;
         const uint32_t *coef;
+        // k_texec form: U slots register-allocated to nu LDS slots; the term streams
+        const DevSrc *tsrcs, *tdsts;
+        uint32_t nu;
+        const uint4 *terms;
+        const uint32_t *wbeg;         // term ranges per (level, wave)
+        uint32_t nwv;                 // waves per workgroup the streams were cut for
     };
     std::map<std::pair<const Plan *, int>, DevGrouped> gplan;
     std::map<int, uint32_t *> mtab;
@@ -650,6 +781,21 @@ static Error upload_vec(const std::vector<T> &v, const T **out) {
 }
 
 // Device copy of a plan's groups (once per plan and device; plans are never freed).
+// Waves per workgroup of the tile-fused executor: enough for the widest level's groups
+// (4 / 8 / 16), or CLAY_TEXEC_WAVES.
+static uint32_t texec_waves(const Plan &pl) {
+    static const int forced = [] {
+        const char *e = getenv("CLAY_TEXEC_WAVES");
+        const int v = e ? atoi(e) : 0;
+        return v == 4 || v == 8 || v == 16 ? v : 0;
+    }();
+    if (forced) return uint32_t(forced);
+    uint32_t mx = 0;
+    for (size_t L = 0; L + 1 < pl.gstage_begin.size(); L++)
+        mx = std::max(mx, pl.gstage_begin[L + 1] - pl.gstage_begin[L]);
+    return mx <= 8 ? 4u : mx <= 16 ? 8u : 16u;
+}
+
 static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::DevGrouped *out) {
     std::lock_guard<std::mutex> lk(cs.mu);
     auto key = std::make_pair(&pl, dev);
@@ -660,6 +806,92 @@ static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::De
         if (!e) e = upload_vec(pl.gsrcs, &g.srcs);
         if (!e) e = upload_vec(pl.gdsts, &g.dsts);
         if (!e) e = upload_vec(pl.gcoef, &g.coef);
+        if (e) return e;
+        // U slots of the tile-fused executor: register-allocated by level.  A slot is live
+        // from the level that writes it through the last level that reads it; an LDS slot
+        // is reused only by a later level than every reader of its previous value (a level
+        // runs on all waves at once, so same-level reuse would race).
+        std::vector<DevSrc> ts(pl.gsrcs), td(pl.gdsts);
+        const uint32_t ub = 2 * pl.tn;
+        const size_t nst = pl.gstage_begin.size() - 1;
+        std::map<uint32_t, size_t> last_read;
+        for (size_t L = 0; L < nst; L++)
+            for (uint32_t gi = pl.gstage_begin[L]; gi < pl.gstage_begin[L + 1]; gi++) {
+                const DevGroup &dg = pl.groups[gi];
+                for (uint32_t j = 0; j < dg.nsrc; j++)
+                    if (pl.gsrcs[dg.src_begin + j].base == ub) last_read[pl.gsrcs[dg.src_begin + j].slot] = L;
+            }
+        std::map<uint32_t, uint32_t> phys;  // plan slot -> LDS slot
+        std::vector<uint32_t> free_slots;
+        std::vector<std::pair<size_t, uint32_t>> busy;  // (last read level, LDS slot)
+        uint32_t nphys = 0;
+        for (size_t L = 0; L < nst; L++) {
+            for (size_t i = 0; i < busy.size();) {  // values no level >= L reads
+                if (busy[i].first < L) {
+                    free_slots.push_back(busy[i].second);
+                    busy[i] = busy.back();
+                    busy.pop_back();
+                } else {
+                    i++;
+                }
+            }
+            for (uint32_t gi = pl.gstage_begin[L]; gi < pl.gstage_begin[L + 1]; gi++) {
+                const DevGroup &dg = pl.groups[gi];
+                for (uint32_t j = 0; j < dg.ndst; j++) {
+                    const DevSrc &d = pl.gdsts[dg.dst_begin + j];
+                    if (d.base != ub || phys.count(d.slot)) continue;
+                    uint32_t p;
+                    if (!free_slots.empty()) {
+                        p = free_slots.back();
+                        free_slots.pop_back();
+                    } else {
+                        p = nphys++;
+                    }
+                    phys[d.slot] = p;
+                    auto lr = last_read.find(d.slot);
+                    busy.emplace_back(lr == last_read.end() ? L : lr->second, p);
+                }
+            }
+        }
+        g.nu = nphys;
+        for (auto *v : {&td, &ts})
+            for (auto &x : *v)
+                if (x.base == ub) {
+                    auto it = phys.find(x.slot);
+                    if (it == phys.end()) g.nu = UINT32_MAX;  // read before any write: never tile-run
+                    else x.slot = it->second;
+                }
+        // term streams (k_texec): level L, wave w runs groups gstage_begin[L] + w + i * nwv
+        const uint32_t nwv = texec_waves(pl);
+        std::vector<uint4> terms;
+        std::vector<uint32_t> wbeg;
+        for (size_t L = 0; L < nst; L++)
+            for (uint32_t w = 0; w < nwv; w++) {
+                wbeg.push_back(uint32_t(terms.size()));
+                for (uint32_t gi = pl.gstage_begin[L] + w; gi < pl.gstage_begin[L + 1]; gi += nwv) {
+                    const DevGroup &dg = pl.groups[gi];
+                    for (uint32_t j = 0; j < dg.nsrc; j++) {
+                        const DevSrc &x = ts[dg.src_begin + j];
+                        if (x.base > 255 || x.slot > 0xFFFFFFu || dg.dst_begin > 0xFFFFFFu || dg.ndst > 8)
+                            g.nu = UINT32_MAX;  // not encodable: never tile-run
+                        uint4 r;
+                        r.x = x.base << 24 | (x.slot & 0xFFFFFFu);
+                        r.y = r.w = 0;
+                        r.z = dg.ndst << 24 | (j + 1 == dg.nsrc ? (1u << 31) | (dg.dst_begin & 0xFFFFFFu) : 0u);
+                        for (uint32_t d = 0; d < dg.ndst && d < 8; d++) {
+                            const uint32_t c = pl.gcoef[dg.coef_begin + d * dg.nsrc + j] & 0xFFu;
+                            (d < 4 ? r.y : r.w) |= c << (8 * (d & 3));
+                        }
+                        terms.push_back(r);
+                    }
+                }
+            }
+        wbeg.push_back(uint32_t(terms.size()));
+        g.nwv = nwv;
+        e = upload_vec(ts, &g.tsrcs);
+        if (!e) e = upload_vec(td, &g.tdsts);
+        if (!e) e = upload_vec(terms, &g.terms);
+        if (!e) e = upload_vec(wbeg, &g.wbeg);
         if (e) return e;
         it = cs.gplan.emplace(key, g).first;
     }
@@ -731,13 +963,92 @@ static int align_of(uintptr_t p) {
     return 1;
 }
 
-// Execute a plan: C/H/OUT pointer bindings given, U workspace bound here.  One k_gexec
-// launch per dependency level; 16 bytes per lane regardless of sc / pointer alignment.
+// Executor selection (clay_set_exec_mode): process-wide, read without locks.
+enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2 };
+static std::atomic<int> g_exec_mode{kExecAuto};
+static size_t tex_lds_budget() {
+    static const size_t b = [] {
+        const char *e = getenv("CLAY_TEXEC_LDS_KB");
+        return size_t(e ? atoi(e) : 80) * 1024;
+    }();
+    return b;
+}
+// Lane width of the tile-fused executor for a plan (0 = not eligible): the widest of
+// 16 / 8 / 4 bytes whose tile of U slots (nu x 64 x VW) fits the LDS budget (default
+// 80 KiB: two workgroups per CU); failing that, 4-byte lanes with up to 160 KiB (one
+// workgroup per CU) when CLAY_TEXEC_BIG=1.
+static int texec_vw(const Plan &pl, uint32_t nu, uint32_t maxd) {
+    const size_t stages = pl.gstage_begin.size() - 1;
+    if (stages == 0 || stages > size_t(kTexMaxStages) || maxd > 8 || nu == UINT32_MAX) return 0;
+    for (int vw = 16; vw >= 4; vw >>= 1)
+        if (uint64_t(nu) * 64 * vw + kTexTabBytes <= tex_lds_budget()) return vw;
+    static const bool big = [] {
+        const char *e = getenv("CLAY_TEXEC_BIG");
+        return e && atoi(e) != 0;
+    }();
+    if (big && uint64_t(nu) * 64 * 4 + kTexTabBytes <= kTexLdsMax) return 4;
+    return 0;
+}
+template <int VW, int MAXD, int NWV>
+static Error launch_texec2(const ExecPtrs &ptrs, const CodeState::DevGrouped &g, const uint32_t *tabs,
+                           uint32_t nstages, uint64_t sc, uint32_t ubase, hipStream_t stream, int dev) {
+    const size_t lds = size_t(g.nu) * 64 * VW + kTexTabBytes;
+    Error e = lds_attr_once(reinterpret_cast<const void *>(&k_texec<VW, MAXD, NWV>), int(kTexLdsMax), dev);
+    if (e) return e;
+    const uint64_t tiles = (sc + 64 * VW - 1) / (64 * VW);
+    k_texec<VW, MAXD, NWV><<<dim3(uint32_t(tiles)), dim3(64 * NWV), lds, stream>>>(ptrs, g.terms, g.wbeg, tabs,
+                                                                                  g.tdsts, nstages, sc, ubase, g.nu);
+    CLAY_HIP(hipGetLastError());
+    return Error{};
+}
+template <int VW, int MAXD>
+static Error launch_texec1(const ExecPtrs &ptrs, const CodeState::DevGrouped &g, const uint32_t *tabs,
+                           uint32_t nstages, uint64_t sc, uint32_t ubase, hipStream_t stream, int dev) {
+    if (g.nwv == 4) return launch_texec2<VW, MAXD, 4>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+    if (g.nwv == 8) return launch_texec2<VW, MAXD, 8>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+    return launch_texec2<VW, MAXD, 16>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+}
+template <int VW>
+static Error launch_texec(uint32_t maxd, const ExecPtrs &ptrs, const CodeState::DevGrouped &g, const uint32_t *tabs,
+                          uint32_t nstages, uint64_t sc, uint32_t ubase, hipStream_t stream, int dev) {
+    if (maxd <= 1) return launch_texec1<VW, 1>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+    if (maxd <= 2) return launch_texec1<VW, 2>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+    if (maxd <= 4) return launch_texec1<VW, 4>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+    return launch_texec1<VW, 8>(ptrs, g, tabs, nstages, sc, ubase, stream, dev);
+}
+
+// Execute a plan: C/H/OUT pointer bindings given, U workspace bound here.  The
+// tile-fused executor (one launch, U in LDS) where the plan's U slots fit, else one
+// k_gexec launch per dependency level; 16 bytes per lane regardless of sc / pointer
+// alignment.
 static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
                       ExecPtrs ptrs, size_t sc, size_t chunk_for_ws) {
     CodeState::DevGrouped g{};
     Error e = upload_groups(cs, pl, dev, &g);
     if (e) return e;
+    const int xm = g_exec_mode.load(std::memory_order_relaxed);
+    // auto: the tile executor only for small plans (at most kTexAutoGroups groups), where
+    // the grouped executor's launches are latency-bound -- (4,2,5) decode 64 MiB: 0.043 ->
+    // 0.038 ms.  On the big plans it measured slower than the grouped executor ((9,3,11)
+    // repair 0.53 vs 0.43 ms, (10,4,13) 1-erasure decode 0.72 vs 0.41 ms),
+    // so "tile" mode runs it wherever eligible but auto does not.
+    const bool tex_ok = xm == kExecTile || (xm == kExecAuto && pl.groups.size() <= kTexAutoGroups);
+    if (tex_ok && sc > 0 && sc / (64 * 4) < 0x7fffffffu) {
+        uint32_t maxd = 1;
+        for (uint32_t m : pl.gstage_maxd) maxd = std::max(maxd, m);
+        const int vw = texec_vw(pl, g.nu, maxd);
+        static const bool dbg = getenv("CLAY_PLAN_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "run_plan: %zu levels, %u LDS U slots, maxd %u -> tile executor vw %d\n",
+                         pl.gstage_begin.size() - 1, g.nu, maxd, vw);
+        if (vw) {
+            const uint32_t nst = uint32_t(pl.gstage_begin.size() - 1), ub = 2 * pl.tn;
+            e = vw == 16 ? launch_texec<16>(maxd, ptrs, g, ds.d_tabs, nst, sc, ub, stream, dev)
+              : vw == 8  ? launch_texec<8>(maxd, ptrs, g, ds.d_tabs, nst, sc, ub, stream, dev)
+                         : launch_texec<4>(maxd, ptrs, g, ds.d_tabs, nst, sc, ub, stream, dev);
+            if (!e) t_last_launches += 1;
+            return e;
+        }
+    }
     LeaseGuard ws(ds, stream);
     if (pl.uses_u) {
         e = lease_acquire(ds, size_t(pl.tn) * chunk_for_ws, stream, &ws.l);
@@ -1478,6 +1789,10 @@ int clay_set_encode_path(int mode) {
     g_encode_tile.store(tile);
     g_encode_mode.store(path);
     return prev;
+}
+int clay_set_exec_mode(int mode) {
+    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile) return -1;
+    return g_exec_mode.exchange(mode);
 }
 const char *clay_last_encode_path(void) { return t_last_path.c_str(); }
 size_t clay_last_launch_count(void) { return t_last_launches; }

@@ -247,6 +247,17 @@ size_t clay_workspace_bytes(int device);
  * Returns the previous setting (path | variant << 8). */
 int clay_set_encode_path(int mode);
 
+/* Plan executor for decode, repair and the staged encode (process-wide tuning knob; no
+ * reference counterpart -- the crate has one CPU path):
+ *   0 auto    -- the tile-fused executor (one launch, U workspace in LDS) for small plans
+ *                (<= 32 op groups) whose U slots fit the LDS budget, else the grouped
+ *                per-level executor
+ *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
+ *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
+ * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
+ * unknown mode (setting unchanged). */
+int clay_set_exec_mode(int mode);
+
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
 const char *clay_last_encode_path(void);
 

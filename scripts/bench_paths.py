@@ -17,6 +17,8 @@ import clay_amd  # noqa: E402
 from clay_amd import ClayCode  # noqa: E402
 
 RUNS = int(os.environ.get("RUNS", "10"))
+EXEC = os.environ.get("CLAY_EXEC", "auto")  # plan executor: auto | grouped | tile
+clay_amd.set_exec_mode(EXEC)
 stream = torch.cuda.current_stream()
 
 
@@ -37,7 +39,7 @@ def report(name, ms, mn, algo, extra=None):
     d = {"config": name, "median_ms": round(ms, 4), "min_ms": round(mn, 4),
          "algorithmic_bytes": int(algo), "GBps": round(algo / (ms * 1e-3) / 1e9, 1),
          "frac_of_8TBps": round(algo / (ms * 1e-3) / 8e12, 4), "path": (clay_amd.last_encode_path() if name.startswith("encode")
-                  else "staged-" + os.environ.get("CLAY_EXEC", "grouped")),
+                  else ("tile" if clay_amd.last_launch_count() == 1 else "grouped")),
          "launches": clay_amd.last_launch_count()}
     if extra:
         d.update(extra)
@@ -118,13 +120,17 @@ def prewarm(ms=250.0):
 
 if __name__ == "__main__":
     prewarm(float(os.environ.get("PREWARM_MS", "250")))
-    encode_cfg(10, 4, 13, 1 << 30)
-    encode_cfg(4, 2, 5, 64 << 20)
-    encode_cfg(9, 3, 11, 9 * (256 << 20))
-    encode_batch_cfg(4, 2, 5, 1 << 20, 256)
-    decode_cfg(4, 2, 5, 64 << 20, [0])
-    decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])
-    decode_cfg(10, 4, 13, 1 << 30, [0])
-    repair_cfg(9, 3, 11, 268_435_458, 0)
-    repair_cfg(9, 3, 11, 268_435_458, 11)
-    repair_cfg(10, 4, 13, 107_374_592, 0)
+    only = os.environ.get("ONLY", "encode,batch,decode,repair").split(",")
+    jobs = [("encode", lambda: encode_cfg(10, 4, 13, 1 << 30)),
+            ("encode", lambda: encode_cfg(4, 2, 5, 64 << 20)),
+            ("encode", lambda: encode_cfg(9, 3, 11, 9 * (256 << 20))),
+            ("batch", lambda: encode_batch_cfg(4, 2, 5, 1 << 20, 256)),
+            ("decode", lambda: decode_cfg(4, 2, 5, 64 << 20, [0])),
+            ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
+            ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0])),
+            ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 0)),
+            ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 11)),
+            ("repair", lambda: repair_cfg(10, 4, 13, 107_374_592, 0))]
+    for tag, fn in jobs:
+        if tag in only:
+            fn()

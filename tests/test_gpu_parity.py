@@ -32,6 +32,14 @@ def _auto_path():
     set_encode_path("auto")
 
 
+@pytest.fixture(params=["tile", "grouped"])
+def exec_mode(request):
+    """Run a decode/repair test under both plan executors (tile-fused and grouped)."""
+    prev = clay_amd.set_exec_mode(request.param)
+    yield request.param
+    clay_amd.set_exec_mode(prev)
+
+
 @pytest.mark.parametrize("cfg", CONFIGS)
 @pytest.mark.parametrize("size_kind", ["empty", "tiny", "ragged", "aligned16", "sc2", "big"])
 def test_encode_matches_oracle(oracle_mod, cfg, size_kind):
@@ -120,7 +128,7 @@ def test_encode_path_rejects_unknown_variants():
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_encode_fused_equals_staged(oracle_mod, cfg):
+def test_encode_fused_equals_staged(oracle_mod, cfg, exec_mode):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     data = rand_bytes(7, k * c.sub_chunk_no * 2 * 16 - 5)  # sc = 32: fused-eligible
@@ -138,7 +146,7 @@ def test_encode_fused_equals_staged(oracle_mod, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_decode_random_inputs_match_oracle(oracle_mod, cfg):
+def test_decode_random_inputs_match_oracle(oracle_mod, cfg, exec_mode):
     """Non-codeword inputs: only the reference's exact RS row choice reproduces these bytes."""
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
@@ -153,7 +161,7 @@ def test_decode_random_inputs_match_oracle(oracle_mod, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_decode_roundtrip_max_erasures(oracle_mod, cfg):
+def test_decode_roundtrip_max_erasures(oracle_mod, cfg, exec_mode):
     k, m, d = cfg
     c = ClayCode(k, m, d)
     data = rand_bytes(3, k * c.sub_chunk_no * 4 + 9)
@@ -164,7 +172,7 @@ def test_decode_roundtrip_max_erasures(oracle_mod, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_repair_every_node_matches_oracle(oracle_mod, cfg):
+def test_repair_every_node_matches_oracle(oracle_mod, cfg, exec_mode):
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     data = rand_bytes(5, k * c.sub_chunk_no * 2 * 3)
@@ -182,6 +190,37 @@ def test_repair_every_node_matches_oracle(oracle_mod, cfg):
         # random helper payloads: byte-identical to the reference's repair arithmetic
         pr = {h: rng.integers(0, 256, v.size, dtype=np.uint8) for h, v in pd.items()}
         assert c.repair(lost, pr, chunk) == o.repair(lost, pr, chunk), (cfg, lost)
+
+
+@pytest.mark.parametrize("cfg,lost,mode,launches", [((9, 3, 11), 0, "tile", 1), ((4, 2, 5), 3, "auto", 1),
+                                                     ((10, 4, 13), 0, "tile", 1), ((9, 3, 11), 0, "auto", 2)])
+def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
+    """'tile' runs repair plans whose U slots fit in LDS as ONE tile-fused launch, 'auto'
+    only small plans; the bytes equal the grouped executor's and the oracle's."""
+    k, m, d = cfg
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    sc = 16 * 100 + 6
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(77)
+    avail = [i for i in range(c.n) if i != lost]
+    info = c.minimum_to_repair(lost, avail)
+    pr = {h: rng.integers(0, 256, len(idx) * sc, dtype=np.uint8) for h, idx in info}
+    prev = clay_amd.set_exec_mode(mode)
+    try:
+        got = c.repair(lost, pr, chunk)
+        assert clay_amd.last_launch_count() == launches
+        clay_amd.set_exec_mode("grouped")
+        assert c.repair(lost, pr, chunk) == got
+        assert clay_amd.last_launch_count() > 1
+    finally:
+        clay_amd.set_exec_mode(prev)
+    assert got == o.repair(lost, pr, chunk)
+
+
+def test_exec_mode_rejects_unknown():
+    with pytest.raises(ValueError):
+        clay_amd.set_exec_mode("fused")
+    assert clay_amd._lib.lib().clay_set_exec_mode(7) == -1
 
 
 def test_repair_with_all_helpers_and_aloof(oracle_mod):
@@ -414,7 +453,7 @@ def test_cfg3_9_3_11_repair_256MiB_chunks(oracle_mod, torch_cuda, lost):
 
 @pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13)])
 @pytest.mark.parametrize("sc", [16 * 257 + 2, 16 * 1000 + 9, 16 * 3001])
-def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc):
+def test_decode_repair_multi_tile_unaligned_subchunks(oracle_mod, cfg, sc, exec_mode):
     """Sub-chunks spanning several executor tiles whose regions start at 2-byte / odd
     offsets (the (9,3,11) 256 MiB chunk has sc = 3,314,018): random (non-codeword)
     inputs, decode and repair byte-identical to the oracle."""
@@ -458,7 +497,7 @@ def test_encode_host_pipelined_matches_oracle(oracle_mod, torch_cuda, cfg, sc, p
 
 
 @pytest.mark.parametrize("cfg", [(4, 2, 5), (9, 3, 11), (10, 4, 13), (6, 3, 8)])
-def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg):
+def test_repair_device_full_chunks_matches_oracle(oracle_mod, torch_cuda, cfg, exec_mode):
     """Repair straight from whole helper chunks in HBM (no gather): same bytes as the
     oracle's repair on the gathered beta sub-chunks, for codewords and random chunks."""
     torch = torch_cuda
