@@ -148,6 +148,7 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
             for (int d = 0; d < MAXD; d++) {
                 if (d >= int(g.ndst)) break;
                 const uint32_t c = gcoef[g.coef_begin + d * g.nsrc + s];
+                if (c == 0) continue;  // merged groups: source absent from this row
                 if (c == 1) {
 #pragma unroll
                     for (int w = 0; w < NW; w++) acc[d][w] ^= v[b].w[w];
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(64 * NWV) void k_texec(ExecPtrs P, const uint4 *__r
                 for (int d = 0; d < MAXD; d++) {
                     if (d >= int(nd)) break;
                     const uint32_t c = ((d < 4 ? rec[b].y : rec[b].w) >> (8 * (d & 3))) & 0xFFu;
+                    if (c == 0u) continue;
                     if (c == 1u) {
 #pragma unroll
                         for (int w = 0; w < NW; w++) acc[d][w] ^= v[b].w[w];
@@ -1032,7 +1034,8 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     // 0.038 ms.  On the big plans it measured slower than the grouped executor ((9,3,11)
     // repair 0.53 vs 0.43 ms, (10,4,13) 1-erasure decode 0.72 vs 0.41 ms),
     // so "tile" mode runs it wherever eligible but auto does not.
-    const bool tex_ok = xm == kExecTile || (xm == kExecAuto && pl.groups.size() <= kTexAutoGroups);
+    const bool tex_ok = xm == kExecTile || (xm == kExecAuto && pl.groups.size() <= kTexAutoGroups &&
+                                             pl.gstage_begin.size() > 2);  // one level: nothing to fuse
     if (tex_ok && sc > 0 && sc / (64 * 4) < 0x7fffffffu) {
         uint32_t maxd = 1;
         for (uint32_t m : pl.gstage_maxd) maxd = std::max(maxd, m);

@@ -96,13 +96,34 @@ void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
             if (t.ver >= 0 && std::find(rl[t.ver].begin(), rl[t.ver].end(), rslot(o.dst)) == rl[t.ver].end())
                 rl[t.ver].push_back(rslot(o.dst));
     const GF &gf = GF::get();
+    static const int dup_env = [] {
+        const char *e = getenv("CLAY_PLAN_DUP");
+        return e ? atoi(e) : -1;
+    }();
+    const size_t dup_max = size_t(dup_env >= 0 ? dup_env : dup_cost);
+    // all sources of op p are final versions (nothing rewrites them afterwards)
+    auto final_srcs = [&](size_t p) {
+        for (const auto &t : ops[p].src) {
+            auto it = cur.find(t.key);
+            if (t.ver < 0 ? written.count(t.key) != 0 : (it == cur.end() || it->second != t.ver)) return false;
+        }
+        return true;
+    };
     for (size_t i = 0; i < n; i++) {
+        // duplication (dup_max > 0): a <= 2-source output op also substitutes a producer that other
+        // ops still read, when the producer's <= dup_max sources are final -- the op moves
+        // to the producer's level and group_ops' merge puts it into the producer's group
+        // (one extra source), instead of a separate level re-reading the materialised value
+        const bool small = dup_max > 0 && is_out[i] && ops[i].src.size() <= 2;
+        auto subst = [&](const Term &t) {
+            return t.ver >= 0 && (inl[t.ver] || (small && ops[t.ver].src.size() <= dup_max && final_srcs(t.ver)));
+        };
         bool any = false;
-        for (const auto &t : ops[i].src) any |= t.ver >= 0 && inl[t.ver];
+        for (const auto &t : ops[i].src) any |= subst(t);
         if (any) {
             std::vector<Term> nt;
             for (const auto &t : ops[i].src) {
-                if (t.ver >= 0 && inl[t.ver]) {
+                if (subst(t)) {
                     for (const auto &u : ops[t.ver].src) nt.push_back(Term{u.key, u.ver, gf.mul(t.coef, u.coef)});
                 } else {
                     nt.push_back(t);
@@ -212,6 +233,7 @@ std::unique_ptr<Plan> PlanBuilder::finalize(const std::vector<uint64_t> &outputs
         }
         plan->stage_begin.push_back(uint32_t(plan->ops.size()));
     }
+    plan->merge_slack = merge_slack;
     plan->group_ops();
     return plan;
 }
@@ -257,6 +279,44 @@ void Plan::group_ops() {
             std::vector<uint32_t> cf;
             for (auto &x : t) cf.push_back(x.second);
             gs[gi].coef.push_back(cf);
+        }
+        // Near-identical source sets (merge_slack > 0): fold group b into group a when the
+        // union adds at most merge_slack sources to the larger set, so e.g. repair's three
+        // folded outputs of one layer (15 shared helper reads + one own companion each)
+        // share one source pass; the merged coefficient rows hold 0 for absent sources.
+        static const int slack_env = [] {
+            const char *e = getenv("CLAY_PLAN_MERGE_SLACK");
+            return e ? atoi(e) : -1;
+        }();
+        const size_t slack = size_t(slack_env >= 0 ? slack_env : merge_slack);
+        if (slack > 0 && gs.size() > 1) {
+            std::vector<uint8_t> gone(gs.size(), 0);
+            for (size_t a = 0; a < gs.size(); a++) {
+                if (gone[a] || gs[a].src.empty()) continue;
+                for (size_t b = a + 1; b < gs.size(); b++) {
+                    if (gone[b] || gs[b].src.empty() || gs[a].dst.size() + gs[b].dst.size() > kMaxGroupDst) continue;
+                    std::vector<std::pair<uint32_t, uint32_t>> u;
+                    std::set_union(gs[a].src.begin(), gs[a].src.end(), gs[b].src.begin(), gs[b].src.end(),
+                                   std::back_inserter(u));
+                    if (u.size() > std::max(gs[a].src.size(), gs[b].src.size()) + slack) continue;
+                    // re-align both groups' coefficient rows to the union
+                    G m{u, {}, {}};
+                    for (G *x : {&gs[a], &gs[b]})
+                        for (size_t d = 0; d < x->dst.size(); d++) {
+                            std::vector<uint32_t> row(u.size(), 0);
+                            for (size_t j = 0; j < x->src.size(); j++)
+                                row[size_t(std::lower_bound(u.begin(), u.end(), x->src[j]) - u.begin())] = x->coef[d][j];
+                            m.dst.push_back(x->dst[d]);
+                            m.coef.push_back(row);
+                        }
+                    gs[a] = std::move(m);
+                    gone[b] = 1;
+                }
+            }
+            std::vector<G> kept;
+            for (size_t a = 0; a < gs.size(); a++)
+                if (!gone[a]) kept.push_back(std::move(gs[a]));
+            gs = std::move(kept);
         }
         static const bool dbg = getenv("CLAY_PLAN_DEBUG") != nullptr;
         if (dbg) {
@@ -487,6 +547,7 @@ Error plan_encode(const clay_code_t &c, RsCtx &rs, std::unique_ptr<Plan> &out) {
 Error plan_decode(const clay_code_t &c, RsCtx &rs, const std::vector<uint8_t> &er, const std::vector<uint8_t> &want,
                   std::unique_ptr<Plan> &out) {
     PlanBuilder b;
+    b.fold_cost = 24;
     init_zero_inputs(c, b);
     Error e = replay_layered(c, rs, b, er);
     if (e) return e;
@@ -510,6 +571,8 @@ Error plan_repair(const clay_code_t &c, RsCtx &rs, size_t lost, const std::vecto
     const size_t li = internal_of(c, lost), lost_y = li / q;
     const uint8_t g1 = 1, gm = kGamma, det = gamma_det(), ginv = gamma_inv();
     PlanBuilder b;
+    b.fold_cost = 24;
+    b.merge_slack = 2;
     init_zero_inputs(c, b);
     // helper_internal: real helpers + shortened nodes as zero helpers (repair.rs:258-261)
     std::vector<uint8_t> helper(tn, 0), aloof(tn, 0), base(tn, 0);

