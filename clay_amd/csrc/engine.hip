@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                                                       uint32_t tiles, uint64_t sc, uint64_t r0, uint64_t r1,
                                                       uint32_t ngroups, uint32_t order, uint32_t bx,
                                                       uint8_t *const *__restrict__ ptab, uint32_t lps,
-                                                      uint32_t nstripes, const ExecStride S) {
+                                                      uint32_t nstripes, const ExecStride S, uint32_t tpw) {
     constexpr int NW = (VW + 3) / 4;
     // Block -> (group, tile).  order 0: group-major.  1: tile-major -- all groups of a
     // tile run back to back, so an input sub-chunk tile read by several groups is
@@ -97,7 +97,9 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
         if (threadIdx.x >= spb * lps || stripe >= nstripes) return;
     }
     const DevGroup g = groups[g0 + gi];
-    const uint64_t pos = r0 + (uint64_t(tile) * lps + lane) * VW;
+    // tpw consecutive tiles per block (one group's scalar work amortised over tpw tiles)
+    for (uint32_t tk = 0; tk < tpw; tk++) {
+    const uint64_t pos = r0 + ((uint64_t(tile) * tpw + tk) * lps + lane) * VW;
     if (pos >= r1) return;
     // Regions start at slot*sc, which is only 2-byte aligned for e.g. the (9,3,11)
     // chunk of 268,435,458 B; gfx950 global loads/stores run in unaligned mode, so
@@ -199,6 +201,7 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
             for (uint32_t i = 0; i < nb; i++) dp[i] = tb[i];
         }
     }
+    }  // tiles of the block
 }
 
 
@@ -950,7 +953,8 @@ template <int VW, int MAXD>
 static void launch_gexec1(int mode, dim3 grid, dim3 block, hipStream_t stream, const ExecPtrs &ptrs,
                           const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
                           uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n, uint32_t order, uint32_t bx,
-                          uint8_t *const *ptab, uint32_t lps, uint32_t nstripes, const ExecStride &S) {
+                          uint8_t *const *ptab, uint32_t lps, uint32_t nstripes, const ExecStride &S,
+                          uint32_t tpw) {
     // software-pipelined source loads (default; CLAY_GEXEC_PIPE=0 disables): repair (9,3,11)
     // 0.330 -> 0.323 ms, decode 4 erasures 0.863 -> 0.855 ms (profiles/r02/gexec_pipe.txt)
     static const bool pipe = [] {
@@ -961,14 +965,14 @@ static void launch_gexec1(int mode, dim3 grid, dim3 block, hipStream_t stream, c
            : mode == kBatchAffine ? k_gexec<VW, MAXD, kBatchAffine>
            : pipe ? k_gexec<VW, MAXD, kBatchNone, true> : k_gexec<VW, MAXD, kBatchNone>;
     k<<<grid, block, 0, stream>>>(ptrs, g.groups, g.srcs, g.dsts, g.coef, tabs, b, tiles, sc, r0, r1, n, order, bx,
-                                  ptab, lps, nstripes, S);
+                                  ptab, lps, nstripes, S, tpw);
 }
 template <int VW>
 static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const ExecPtrs &ptrs,
                          const CodeState::DevGrouped &g, const uint32_t *tabs, uint32_t b, uint32_t tiles,
                          uint64_t sc, uint64_t r0, uint64_t r1, uint32_t n, int mode = kBatchNone,
                          uint8_t *const *ptab = nullptr, const ExecStride *stride = nullptr, uint32_t nstripes = 1,
-                         uint32_t lps = kExecBlock) {
+                         uint32_t lps = kExecBlock, uint32_t tpw = 1) {
     dim3 block(kExecBlock);
     static const uint32_t order = [] {
         const char *e = getenv("CLAY_GEXEC_ORDER");
@@ -980,10 +984,10 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
     if (order == 2) grid = dim3(8 * bx);
     const uint32_t spb = kExecBlock / lps;
     grid.y = (nstripes + spb - 1) / spb;
-    if (maxd <= 1) launch_gexec1<VW, 1>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
-    else if (maxd <= 2) launch_gexec1<VW, 2>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
-    else if (maxd <= 4) launch_gexec1<VW, 4>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
-    else launch_gexec1<VW, 8>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S);
+    if (maxd <= 1) launch_gexec1<VW, 1>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S, tpw);
+    else if (maxd <= 2) launch_gexec1<VW, 2>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S, tpw);
+    else if (maxd <= 4) launch_gexec1<VW, 4>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S, tpw);
+    else launch_gexec1<VW, 8>(mode, grid, block, stream, ptrs, g, tabs, b, tiles, sc, r0, r1, n, order, bx, ptab, lps, nstripes, S, tpw);
 }
 
 static int align_of(uintptr_t p) {
@@ -1086,13 +1090,25 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
         ptrs.p[2 * pl.tn] = ws.ptr();
     }
     size_t launches = 0;
-    const uint32_t tiles = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+    // consecutive 4 KiB tiles per block: 2 for deep plans (>= 4 levels: multi-erasure
+    // decodes, whose many small groups amortise their per-block scalar work over two
+    // tiles: (10,4,13) 4 erasures 1.026 -> 0.964 ms on one box), else 1 (4 and 8 measured
+    // slower everywhere; profiles/r02/gexec_tpw.txt).  CLAY_GEXEC_TPW overrides.
+    static const int tpw_env = [] {
+        const char *e = getenv("CLAY_GEXEC_TPW");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 64 ? v : 0;
+    }();
+    const uint32_t tpw = tpw_env ? uint32_t(tpw_env) : (pl.gstage_begin.size() >= 5 ? 2u : 1u);
+    const uint32_t tiles1 = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+    const uint32_t tiles = (tiles1 + tpw - 1) / tpw;
     for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
         uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
         const uint32_t maxd = pl.gstage_maxd[s];
         while (b < end) {
             uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
-            launch_gexec<16>(maxd, dim3(n * tiles), stream, ptrs, g, ds.d_tabs, b, tiles, sc, 0, sc, n);
+            launch_gexec<16>(maxd, dim3(n * tiles), stream, ptrs, g, ds.d_tabs, b, tiles, sc, 0, sc, n, kBatchNone,
+                             nullptr, nullptr, 1, kExecBlock, tpw);
             CLAY_HIP(hipGetLastError());
             launches++;
             b += n;
