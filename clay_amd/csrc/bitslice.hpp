@@ -224,6 +224,10 @@ struct BsArgs {
     uint8_t *par[8];                 // parity y-section, node x (internal (t-1)q + x)
     uint64_t sc;                     // sub-chunk bytes, multiple of 8
     uint32_t ntiles, tiles_per_xcd, nslots;
+    // k_bs_encode batches: stripe s's nodes at data[i] + s * sdata, par[x] + s * spar
+    // (ntiles tiles per stripe, tiles_per_xcd over all nstripes * ntiles); 0 = one stripe
+    uint32_t nstripes;
+    int64_t sdata, spar;
 };
 
 // Code shape derived at compile time from (k, m) with d = k + m - 1 (q = m).
@@ -293,7 +297,7 @@ struct BsKernel {
 
     // ---- phase A, one y-section ----
     template <int Y, bool FULL>
-    __device__ static void section(const BsArgs &a, uint32_t *lds, uint64_t b0) {
+    __device__ static void section(const BsArgs &a, uint32_t *lds, uint64_t b0, int64_t doff) {
         constexpr int WY = [] { int w = 1; for (int i = 0; i < T - 1 - Y; i++) w *= Q; return w; }();
         for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
             const int pg = u % PG, j = (u / PG) % Q, line = u / (PG * Q);
@@ -305,13 +309,13 @@ struct BsKernel {
             // companion node (Y, j); for j == x or a shortened companion the load is
             // still issued (it hits lines a neighbour lane loads) and masked to zero
             const bool creal = (Y * Q + j) < KD;
-            const uint8_t *cnode = a.data[creal ? Y * Q + j : Y * Q];
+            const uint8_t *cnode = a.data[creal ? Y * Q + j : Y * Q] + doff;
             uint32_t U[Q * 8];
             sfor<Q>([&](auto xc) BS_INL {
                 constexpr int x = decltype(xc)::value;
                 uint32_t o[8], c[8];
                 if constexpr (Y * Q + x < KD) {
-                    ld32<FULL>(o, a.data[Y * Q + x] + lane_off + uint64_t(j) * WY * a.sc, nv);
+                    ld32<FULL>(o, a.data[Y * Q + x] + doff + lane_off + uint64_t(j) * WY * a.sc, nv);
                 } else {
 #pragma unroll
                     for (int w = 0; w < 8; w++) o[w] = 0;
@@ -358,7 +362,7 @@ struct BsKernel {
 
     // ---- phase B: PFT of the parity y-section (digit t-1, weight 1) + store ----
     template <bool FULL>
-    __device__ static void finish(const BsArgs &a, const uint32_t *lds, uint64_t b0) {
+    __device__ static void finish(const BsArgs &a, const uint32_t *lds, uint64_t b0, int64_t poff) {
         for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
             const int pg = u % PG, j = (u / PG) % Q, g = u / (PG * Q);
             const int z0 = g * Q;
@@ -369,7 +373,7 @@ struct BsKernel {
                 uint32_t v[8];
                 read8(lds, j, z0 + j, pg, v);
                 transpose8(v);
-                st32<FULL>(a.par[j] + off, v, nv);
+                st32<FULL>(a.par[j] + poff + off, v, nv);
             }
 #pragma unroll
             for (int k = 1; k < Q; k++) {
@@ -381,18 +385,18 @@ struct BsKernel {
                     c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
                 });
                 transpose8(c);
-                st32<FULL>(a.par[x] + off, c, nv);
+                st32<FULL>(a.par[x] + poff + off, c, nv);
             }
         }
     }
 
     template <bool FULL>
-    __device__ static void tile(const BsArgs &a, uint32_t *lds, uint64_t b0) {
+    __device__ static void tile(const BsArgs &a, uint32_t *lds, uint64_t b0, int64_t doff = 0, int64_t poff = 0) {
         sfor<T - 1>([&](auto yc) BS_INL {
-            section<decltype(yc)::value, FULL>(a, lds, b0);
+            section<decltype(yc)::value, FULL>(a, lds, b0, doff);
             __syncthreads();
         });
-        finish<FULL>(a, lds, b0);
+        finish<FULL>(a, lds, b0, poff);
         __syncthreads();
     }
 };
@@ -402,12 +406,16 @@ __global__ __launch_bounds__((BsKernel<KD, M, PG>::BLOCK)) void k_bs_encode(BsAr
     using Kn = BsKernel<KD, M, PG>;
     __shared__ __attribute__((aligned(16))) uint32_t lds[Kn::LDS_WORDS];
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    const uint32_t ns = a.nstripes ? a.nstripes : 1u, total = a.ntiles * ns;
     for (uint32_t tix = slot; tix < a.tiles_per_xcd; tix += a.nslots) {
-        const uint32_t tile = xcd * a.tiles_per_xcd + tix;
-        if (tile >= a.ntiles) break;
+        // flattened (stripe, tile): each XCD streams a contiguous run of stripes' tiles
+        const uint32_t ft = xcd * a.tiles_per_xcd + tix;
+        if (ft >= total) break;
+        const uint32_t stripe = ft / a.ntiles, tile = ft - stripe * a.ntiles;
         const uint64_t b0 = uint64_t(tile) * Kn::W;
-        if (b0 + Kn::W <= a.sc) Kn::template tile<true>(a, lds, b0);
-        else Kn::template tile<false>(a, lds, b0);
+        const int64_t doff = int64_t(stripe) * a.sdata, poff = int64_t(stripe) * a.spar;
+        if (b0 + Kn::W <= a.sc) Kn::template tile<true>(a, lds, b0, doff, poff);
+        else Kn::template tile<false>(a, lds, b0, doff, poff);
     }
 }
 

@@ -1500,6 +1500,83 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
     return Error{};
 }
 
+// Batched bit-sliced encode (k_bs_encode over nstripes x ntiles flattened tiles, one
+// launch): stripe s = stripe 0's node pointers + s * a uniform data / parity stride.
+template <int KD, int M, int PG>
+static Error launch_bs_batch(CodeState &cs, int dev, const uint8_t *const *data0, uint8_t *const *par0,
+                             int64_t sdata, int64_t spar, size_t ns, size_t sc, hipStream_t stream, bool *done) {
+    using Kn = bs::BsKernel<KD, M, PG>;
+    using S = typename Kn::S;
+    for (int p = 0; p < M; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    const uint64_t ntiles = (sc + Kn::W - 1) / Kn::W;
+    // sub-chunks well under a tile would leave most lanes idle: the staged batch packs them
+    if (sc < uint64_t(Kn::W) / 2 || ntiles * ns >= 0xFFFFFFFFull) return Error{};
+    const int per_cu = std::max(1, int((160 * 1024) / (Kn::LDS_WORDS * 4)));
+    bs::BsArgs a{};
+    for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data0[i] : nullptr;
+    for (int x = 0; x < M; x++) a.par[x] = par0[x];
+    a.sc = sc;
+    a.ntiles = uint32_t(ntiles);
+    a.nstripes = uint32_t(ns);
+    a.sdata = sdata;
+    a.spar = spar;
+    a.tiles_per_xcd = uint32_t((ntiles * ns + 7) / 8);
+    const uint32_t max_slots = uint32_t(std::max(1, dev_props(dev).raw.multiProcessorCount / 8) * per_cu);
+    a.nslots = std::min(max_slots, a.tiles_per_xcd);
+    bs::k_bs_encode<KD, M, PG><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+    CLAY_HIP(hipGetLastError());
+    t_last_launches++;
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "bitsliced-batch-k%dm%d-w%d", KD, M, Kn::W);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+static Error encode_bs_batch(CodeState &cs, int dev, const uint8_t *const *data, uint8_t *const *par, size_t ns,
+                             size_t chunk, hipStream_t stream, const Strided *sd, bool *done) {
+    *done = false;
+    const clay_code_t &c = cs.code;
+    const size_t sc = chunk / c.sub_chunk_no;
+    const int key = int(c.k * 100 + c.m);
+    if (sc % 8 != 0 || c.d != c.k + c.m - 1 || !(key == 402 || key == 804 || key == 903 || key == 603)) return Error{};
+    // stripe-0 pointers and one stride for all data nodes, one for all parity nodes
+    std::vector<const uint8_t *> d0(c.k);
+    std::vector<uint8_t *> p0(c.m);
+    int64_t sdata = 0, spar = 0;
+    auto dptr = [&](size_t s, size_t i) -> const uint8_t * {
+        return sd ? sd->data + int64_t(s) * sd->dstripe + int64_t(i) * sd->dnode : data[s * c.k + i];
+    };
+    auto pptr = [&](size_t s, size_t i) -> uint8_t * {
+        return sd ? sd->par + int64_t(s) * sd->pstripe + int64_t(i) * sd->pnode : par[s * c.m + i];
+    };
+    sdata = int64_t(dptr(1, 0) - dptr(0, 0));
+    spar = int64_t(pptr(1, 0) - pptr(0, 0));
+    for (size_t i = 0; i < c.k; i++) d0[i] = dptr(0, i);
+    for (size_t i = 0; i < c.m; i++) p0[i] = pptr(0, i);
+    if (!sd) {
+        for (size_t s = 0; s < ns; s++) {
+            for (size_t i = 0; i < c.k; i++)
+                if (dptr(s, i) != d0[i] + int64_t(s) * sdata) return Error{};
+            for (size_t i = 0; i < c.m; i++)
+                if (pptr(s, i) != p0[i] + int64_t(s) * spar) return Error{};
+        }
+    }
+    // 8-byte alignment of every stripe's chunks: stripe 0 and both strides
+    auto al8 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; };
+    for (auto p : d0) if (!al8(p)) return Error{};
+    for (auto p : p0) if (!al8(p)) return Error{};
+    if ((sdata & 7) || (spar & 7)) return Error{};
+    switch (key) {
+    case 402: return launch_bs_batch<4, 2, 64>(cs, dev, d0.data(), p0.data(), sdata, spar, ns, sc, stream, done);
+    case 804: return launch_bs_batch<8, 4, 8>(cs, dev, d0.data(), p0.data(), sdata, spar, ns, sc, stream, done);
+    case 903: return launch_bs_batch<9, 3, 6>(cs, dev, d0.data(), p0.data(), sdata, spar, ns, sc, stream, done);
+    default: return launch_bs_batch<6, 3, 16>(cs, dev, d0.data(), p0.data(), sdata, spar, ns, sc, stream, done);
+    }
+}
+
 static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *data, uint8_t *const *par,
                                 size_t n_stripes, size_t chunk, int dev, void *stream, const Strided *sd = nullptr) {
     Error e = check_code(code);
@@ -1527,11 +1604,16 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
                           rs_error_name(cs.rs.init_err));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int mode = g_encode_mode.load(std::memory_order_relaxed), tile = g_encode_tile.load(std::memory_order_relaxed);
-    // many small stripes: one launch per plan level for the whole batch instead of
-    // one launch per stripe (launch-bound below ~4 MiB of data per stripe)
+    // many small stripes: one launch for the whole batch instead of one per stripe
+    // (launch-bound below ~4 MiB of data per stripe) -- the bit-sliced kernel where the
+    // code has one and the stripes sit at uniform strides, else one launch per plan level
     if (mode == kModeAuto && n_stripes >= 4 && code->k * chunk <= (size_t(4) << 20) &&
-        code->q * code->t <= size_t(kMaxTn))
+        code->q * code->t <= size_t(kMaxTn)) {
+        bool done = false;
+        e = encode_bs_batch(cs, dev, data, par, n_stripes, chunk, st, sd, &done);
+        if (e || done) return e;
         return encode_staged_batch(cs, *ds, dev, data, par, n_stripes, chunk, st, sd);
+    }
     std::vector<const uint8_t *> dv;
     std::vector<uint8_t *> pv;
     if (sd) {  // per-stripe kernels below take pointer arrays

@@ -534,7 +534,11 @@ def test_encode_device_batch_small_stripes(oracle_mod, torch_cuda, cfg, sc, n):
     c.encode_device_batch([data[i] for i in range(n * k)], [par[i] for i in range(n * m)], n, chunk)
     torch.cuda.synchronize()
     if k * chunk <= 4 << 20:  # small stripes batch; larger ones keep the per-stripe kernels
-        assert last_encode_path() == "staged-batch"
+        # uniform strides + a bit-sliced kernel + sub-chunks >= half a tile: one
+        # bit-sliced launch; otherwise one staged launch per plan level
+        assert last_encode_path() == "staged-batch" or last_encode_path().startswith("bitsliced-batch")
+        if (k, m) in ((4, 2), (8, 4), (9, 3), (6, 3)) and sc % 8 == 0 and sc >= 1024:
+            assert last_encode_path().startswith("bitsliced-batch"), last_encode_path()
     got = par.cpu().numpy()
     for s in range(n):
         assert np.array_equal(got[s * m:(s + 1) * m], refs[s][k:]), (cfg, sc, n, s)
