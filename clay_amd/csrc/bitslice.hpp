@@ -222,7 +222,7 @@ constexpr int kMaxNodes = 64;
 struct BsArgs {
     const uint8_t *data[kMaxNodes];  // internal nodes 0..K-1 (nullptr: shortened, known zero)
     uint8_t *par[8];                 // parity y-section, node x (internal (t-1)q + x)
-    uint64_t sc;                     // sub-chunk bytes, multiple of 8
+    uint64_t sc;                     // sub-chunk bytes (v1: any; bs6 / stream: multiple of 8)
     uint32_t ntiles, tiles_per_xcd, nslots;
     // k_bs_encode batches: stripe s's nodes at data[i] + s * sdata, par[x] + s * spar
     // (ntiles tiles per stripe, tiles_per_xcd over all nstripes * ntiles); 0 = one stripe
@@ -251,26 +251,35 @@ __device__ __forceinline__ const uint8_t *pick(const uint8_t *const (&p)[Q], int
     return r;
 }
 
-// 32-byte lane load/store (four 8-byte pieces; in a partial tile only `nv` pieces exist)
+// 32-byte lane load/store (four 8-byte pieces; in a partial tile only `nb` bytes exist)
 template <bool FULL>
-__device__ __forceinline__ void ld32(uint32_t (&d)[8], const uint8_t *p, int nv) {
+__device__ __forceinline__ void ld32(uint32_t (&d)[8], const uint8_t *p, int nb) {
+    // nb = valid bytes of the 32 (partial tiles; any sub-chunk size, any alignment:
+    // gfx950 global loads run unaligned, the last partial word is read byte by byte)
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        if (FULL || i < nv) {
+        if (FULL || 8 * i + 8 <= nb) {
             const uint2 v = *reinterpret_cast<const uint2 *>(p + 8 * i);
             d[2 * i] = v.x;
             d[2 * i + 1] = v.y;
         } else {
-            d[2 * i] = 0;
-            d[2 * i + 1] = 0;
+            uint32_t w[2] = {0u, 0u};
+            for (int b = 8 * i; b < nb; b++) w[(b >> 2) & 1] |= uint32_t(p[b]) << (8 * (b & 3));
+            d[2 * i] = w[0];
+            d[2 * i + 1] = w[1];
         }
     }
 }
 template <bool FULL>
-__device__ __forceinline__ void st32(uint8_t *p, const uint32_t (&d)[8], int nv) {
+__device__ __forceinline__ void st32(uint8_t *p, const uint32_t (&d)[8], int nb) {
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-        if (FULL || i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
+    for (int i = 0; i < 4; i++) {
+        if (FULL || 8 * i + 8 <= nb) {
+            *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
+        } else {
+            for (int b = 8 * i; b < nb; b++) p[b] = uint8_t(d[2 * i + ((b >> 2) & 1)] >> (8 * (b & 3)));
+        }
+    }
 }
 
 template <int KD, int M, int PG>
@@ -304,7 +313,7 @@ struct BsKernel {
             const int hi = line / WY, lo = line % WY;
             const int zbase = hi * WY * Q + lo;
             const uint64_t pos = b0 + uint64_t(32 * pg);
-            const int nv = FULL ? 4 : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);
+            const int nv = FULL ? 32 : int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos);  // valid bytes
             const uint64_t lane_off = uint64_t(zbase) * a.sc + pos;
             // companion node (Y, j); for j == x or a shortened companion the load is
             // still issued (it hits lines a neighbour lane loads) and masked to zero
@@ -367,7 +376,7 @@ struct BsKernel {
             const int pg = u % PG, j = (u / PG) % Q, g = u / (PG * Q);
             const int z0 = g * Q;
             const uint64_t pos = b0 + uint64_t(32 * pg);
-            const int nv = FULL ? 4 : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);
+            const int nv = FULL ? 32 : int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos);  // valid bytes
             const uint64_t off = uint64_t(z0 + j) * a.sc + pos;
             {   // red vertex: C = U
                 uint32_t v[8];

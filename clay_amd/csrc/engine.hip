@@ -1330,18 +1330,21 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     *done = false;
     const clay_code_t &c = cs.code;
     const size_t sc = chunk / c.sub_chunk_no;
-    if (sc % 8 != 0 || c.d != c.k + c.m - 1) return Error{};
-    for (size_t s = 0; s < n_stripes; s++) {
+    if (c.d != c.k + c.m - 1) return Error{};
+    // the LDS-DMA kernels (stream, v6) need 8-byte rows: sc % 8 == 0, 8-byte aligned chunks;
+    // the v1 kernel takes any sub-chunk size and alignment (byte-granular partial words)
+    bool rows8 = sc % 8 == 0;
+    for (size_t s = 0; s < n_stripes && rows8; s++) {
         for (size_t i = 0; i < c.k; i++)
-            if (reinterpret_cast<uintptr_t>(data[s * c.k + i]) % 8) return Error{};
+            if (reinterpret_cast<uintptr_t>(data[s * c.k + i]) % 8) rows8 = false;
         for (size_t i = 0; i < c.m; i++)
-            if (reinterpret_cast<uintptr_t>(par[s * c.m + i]) % 8) return Error{};
+            if (reinterpret_cast<uintptr_t>(par[s * c.m + i]) % 8) rows8 = false;
     }
     const DevProps &prop = dev_props(dev);
     Error e;
     const int key = int(c.k * 100 + c.m);
     // streaming kernel (q = 4, t = 4, k 9 / 10): auto's first choice; tile = loader waves
-    if (mode == kModeStream || mode == kModeAuto) {
+    if (rows8 && (mode == kModeStream || mode == kModeAuto)) {
         if (key == 1004 || key == 904) {
             const int l = tile ? tile : 4;
             if (key == 1004)
@@ -1353,8 +1356,10 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
         }
         if (e || *done || mode == kModeStream) return e;
     }
+    if (mode == kModeStream) return e;
     // v6 (column-per-lane, 2-slot ring); tile 4 = 128-byte tiles / 5-slot ring
     if (mode == kModeBs6) {
+        if (!rows8) return e;
         if (key == 1004) {
             if (tile == 4) e = launch_bs6<10, 4, 4>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
             else e = launch_bs6<10, 4, 8>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
@@ -1541,7 +1546,7 @@ static Error encode_bs_batch(CodeState &cs, int dev, const uint8_t *const *data,
     const clay_code_t &c = cs.code;
     const size_t sc = chunk / c.sub_chunk_no;
     const int key = int(c.k * 100 + c.m);
-    if (sc % 8 != 0 || c.d != c.k + c.m - 1 || !(key == 402 || key == 804 || key == 903 || key == 603)) return Error{};
+    if (c.d != c.k + c.m - 1 || !(key == 402 || key == 804 || key == 903 || key == 603)) return Error{};
     // stripe-0 pointers and one stride for all data nodes, one for all parity nodes
     std::vector<const uint8_t *> d0(c.k);
     std::vector<uint8_t *> p0(c.m);
@@ -1564,11 +1569,6 @@ static Error encode_bs_batch(CodeState &cs, int dev, const uint8_t *const *data,
                 if (pptr(s, i) != p0[i] + int64_t(s) * spar) return Error{};
         }
     }
-    // 8-byte alignment of every stripe's chunks: stripe 0 and both strides
-    auto al8 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; };
-    for (auto p : d0) if (!al8(p)) return Error{};
-    for (auto p : p0) if (!al8(p)) return Error{};
-    if ((sdata & 7) || (spar & 7)) return Error{};
     switch (key) {
     case 402: return launch_bs_batch<4, 2, 64>(cs, dev, d0.data(), p0.data(), sdata, spar, ns, sc, stream, done);
     case 804: return launch_bs_batch<8, 4, 8>(cs, dev, d0.data(), p0.data(), sdata, spar, ns, sc, stream, done);
