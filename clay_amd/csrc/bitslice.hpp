@@ -252,32 +252,37 @@ __device__ __forceinline__ const uint8_t *pick(const uint8_t *const (&p)[Q], int
 }
 
 // 32-byte lane load/store (four 8-byte pieces; in a partial tile only `nb` bytes exist)
-template <bool FULL>
-__device__ __forceinline__ void ld32(uint32_t (&d)[8], const uint8_t *p, int nb) {
-    // nb = valid bytes of the 32 (partial tiles; any sub-chunk size, any alignment:
-    // gfx950 global loads run unaligned, the last partial word is read byte by byte)
+template <bool FULL, bool BT = false>
+__device__ __forceinline__ void ld32(uint32_t (&d)[8], const uint8_t *p, int nv) {
+    // !BT: nv = valid 8-byte pieces.  BT (byte tails: sc % 8 != 0 or unaligned chunks):
+    // nv = valid bytes; gfx950 global loads run unaligned, the partial word is read byte
+    // by byte.  Separate instantiations: the byte loop's registers would otherwise cost
+    // the aligned kernel occupancy ((4,2,5) 64 MiB 0.030 -> 0.0345 ms measured).
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        if (FULL || 8 * i + 8 <= nb) {
+        if (FULL || (BT ? 8 * i + 8 <= nv : i < nv)) {
             const uint2 v = *reinterpret_cast<const uint2 *>(p + 8 * i);
             d[2 * i] = v.x;
             d[2 * i + 1] = v.y;
-        } else {
+        } else if (BT) {
             uint32_t w[2] = {0u, 0u};
-            for (int b = 8 * i; b < nb; b++) w[(b >> 2) & 1] |= uint32_t(p[b]) << (8 * (b & 3));
+            for (int b = 8 * i; b < nv; b++) w[(b >> 2) & 1] |= uint32_t(p[b]) << (8 * (b & 3));
             d[2 * i] = w[0];
             d[2 * i + 1] = w[1];
+        } else {
+            d[2 * i] = 0;
+            d[2 * i + 1] = 0;
         }
     }
 }
-template <bool FULL>
-__device__ __forceinline__ void st32(uint8_t *p, const uint32_t (&d)[8], int nb) {
+template <bool FULL, bool BT = false>
+__device__ __forceinline__ void st32(uint8_t *p, const uint32_t (&d)[8], int nv) {
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        if (FULL || 8 * i + 8 <= nb) {
+        if (FULL || (BT ? 8 * i + 8 <= nv : i < nv)) {
             *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(d[2 * i], d[2 * i + 1]);
-        } else {
-            for (int b = 8 * i; b < nb; b++) p[b] = uint8_t(d[2 * i + ((b >> 2) & 1)] >> (8 * (b & 3)));
+        } else if (BT) {
+            for (int b = 8 * i; b < nv; b++) p[b] = uint8_t(d[2 * i + ((b >> 2) & 1)] >> (8 * (b & 3)));
         }
     }
 }
@@ -305,7 +310,7 @@ struct BsKernel {
     }
 
     // ---- phase A, one y-section ----
-    template <int Y, bool FULL>
+    template <int Y, bool FULL, bool BT>
     __device__ static void section(const BsArgs &a, uint32_t *lds, uint64_t b0, int64_t doff) {
         constexpr int WY = [] { int w = 1; for (int i = 0; i < T - 1 - Y; i++) w *= Q; return w; }();
         for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
@@ -313,7 +318,9 @@ struct BsKernel {
             const int hi = line / WY, lo = line % WY;
             const int zbase = hi * WY * Q + lo;
             const uint64_t pos = b0 + uint64_t(32 * pg);
-            const int nv = FULL ? 32 : int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos);  // valid bytes
+            const int nv = FULL ? (BT ? 32 : 4)
+                         : BT ? int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos)                // bytes
+                              : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);  // pieces
             const uint64_t lane_off = uint64_t(zbase) * a.sc + pos;
             // companion node (Y, j); for j == x or a shortened companion the load is
             // still issued (it hits lines a neighbour lane loads) and masked to zero
@@ -324,12 +331,12 @@ struct BsKernel {
                 constexpr int x = decltype(xc)::value;
                 uint32_t o[8], c[8];
                 if constexpr (Y * Q + x < KD) {
-                    ld32<FULL>(o, a.data[Y * Q + x] + doff + lane_off + uint64_t(j) * WY * a.sc, nv);
+                    ld32<FULL, BT>(o, a.data[Y * Q + x] + doff + lane_off + uint64_t(j) * WY * a.sc, nv);
                 } else {
 #pragma unroll
                     for (int w = 0; w < 8; w++) o[w] = 0;
                 }
-                ld32<FULL>(c, cnode + lane_off + uint64_t(x) * WY * a.sc, nv);
+                ld32<FULL, BT>(c, cnode + lane_off + uint64_t(x) * WY * a.sc, nv);
                 const uint32_t keep = (creal && x != j) ? 0xffffffffu : 0u;
                 const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
                 uint32_t t[8];
@@ -370,19 +377,21 @@ struct BsKernel {
     }
 
     // ---- phase B: PFT of the parity y-section (digit t-1, weight 1) + store ----
-    template <bool FULL>
+    template <bool FULL, bool BT>
     __device__ static void finish(const BsArgs &a, const uint32_t *lds, uint64_t b0, int64_t poff) {
         for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
             const int pg = u % PG, j = (u / PG) % Q, g = u / (PG * Q);
             const int z0 = g * Q;
             const uint64_t pos = b0 + uint64_t(32 * pg);
-            const int nv = FULL ? 32 : int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos);  // valid bytes
+            const int nv = FULL ? (BT ? 32 : 4)
+                         : BT ? int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos)                // bytes
+                              : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);  // pieces
             const uint64_t off = uint64_t(z0 + j) * a.sc + pos;
             {   // red vertex: C = U
                 uint32_t v[8];
                 read8(lds, j, z0 + j, pg, v);
                 transpose8(v);
-                st32<FULL>(a.par[j] + poff + off, v, nv);
+                st32<FULL, BT>(a.par[j] + poff + off, v, nv);
             }
 #pragma unroll
             for (int k = 1; k < Q; k++) {
@@ -394,23 +403,23 @@ struct BsKernel {
                     c[decltype(bc)::value] = xor_sel<pft_mask<decltype(bc)::value>(), false>(0u, in);
                 });
                 transpose8(c);
-                st32<FULL>(a.par[x] + poff + off, c, nv);
+                st32<FULL, BT>(a.par[x] + poff + off, c, nv);
             }
         }
     }
 
-    template <bool FULL>
+    template <bool FULL, bool BT>
     __device__ static void tile(const BsArgs &a, uint32_t *lds, uint64_t b0, int64_t doff = 0, int64_t poff = 0) {
         sfor<T - 1>([&](auto yc) BS_INL {
-            section<decltype(yc)::value, FULL>(a, lds, b0, doff);
+            section<decltype(yc)::value, FULL, BT>(a, lds, b0, doff);
             __syncthreads();
         });
-        finish<FULL>(a, lds, b0, poff);
+        finish<FULL, BT>(a, lds, b0, poff);
         __syncthreads();
     }
 };
 
-template <int KD, int M, int PG>
+template <int KD, int M, int PG, bool BT = false>
 __global__ __launch_bounds__((BsKernel<KD, M, PG>::BLOCK)) void k_bs_encode(BsArgs a) {
     using Kn = BsKernel<KD, M, PG>;
     __shared__ __attribute__((aligned(16))) uint32_t lds[Kn::LDS_WORDS];
@@ -423,8 +432,8 @@ __global__ __launch_bounds__((BsKernel<KD, M, PG>::BLOCK)) void k_bs_encode(BsAr
         const uint32_t stripe = ft / a.ntiles, tile = ft - stripe * a.ntiles;
         const uint64_t b0 = uint64_t(tile) * Kn::W;
         const int64_t doff = int64_t(stripe) * a.sdata, poff = int64_t(stripe) * a.spar;
-        if (b0 + Kn::W <= a.sc) Kn::template tile<true>(a, lds, b0, doff, poff);
-        else Kn::template tile<false>(a, lds, b0, doff, poff);
+        if (b0 + Kn::W <= a.sc) Kn::template tile<true, BT>(a, lds, b0, doff, poff);
+        else Kn::template tile<false, BT>(a, lds, b0, doff, poff);
     }
 }
 

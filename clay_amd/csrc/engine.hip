@@ -1237,7 +1237,11 @@ static Error launch_bs(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t
         a.tiles_per_xcd = (a.ntiles + 7) / 8;
         const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
         a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs_encode<KD, M, PG><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+        bool bt = sc % 8 != 0;  // byte tails: unaligned rows or chunks
+        for (int i = 0; i < KD; i++) bt |= (reinterpret_cast<uintptr_t>(a.data[i]) & 7u) != 0;
+        for (int x = 0; x < M; x++) bt |= (reinterpret_cast<uintptr_t>(a.par[x]) & 7u) != 0;
+        if (bt) bs::k_bs_encode<KD, M, PG, true><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+        else bs::k_bs_encode<KD, M, PG><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
         CLAY_HIP(hipGetLastError());
         t_last_launches++;
     }
@@ -1531,7 +1535,11 @@ static Error launch_bs_batch(CodeState &cs, int dev, const uint8_t *const *data0
     a.tiles_per_xcd = uint32_t((ntiles * ns + 7) / 8);
     const uint32_t max_slots = uint32_t(std::max(1, dev_props(dev).raw.multiProcessorCount / 8) * per_cu);
     a.nslots = std::min(max_slots, a.tiles_per_xcd);
-    bs::k_bs_encode<KD, M, PG><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+    bool bt = sc % 8 != 0 || (sdata & 7) != 0 || (spar & 7) != 0;  // byte tails
+    for (int i = 0; i < KD; i++) bt |= (reinterpret_cast<uintptr_t>(a.data[i]) & 7u) != 0;
+    for (int x = 0; x < M; x++) bt |= (reinterpret_cast<uintptr_t>(a.par[x]) & 7u) != 0;
+    if (bt) bs::k_bs_encode<KD, M, PG, true><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+    else bs::k_bs_encode<KD, M, PG><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
     CLAY_HIP(hipGetLastError());
     t_last_launches++;
     char buf[64];
