@@ -198,6 +198,32 @@ std::unique_ptr<Plan> PlanBuilder::finalize(const std::vector<uint64_t> &outputs
             if (s.ver >= 0) max_reader[s.ver] = std::max(max_reader[s.ver], lv);
         max_level = std::max(max_level, lv);
     }
+    // Deferred outputs (defer_outputs / CLAY_PLAN_DEFER_OUT): small ops (<= 2 sources) that
+    // write a final output nothing reads, over final source versions, move from their
+    // earliest level to the last one -- the tail levels fill with independent work
+    // instead of idling at level boundaries.
+    static const int defer_env = [] {
+        const char *e = getenv("CLAY_PLAN_DEFER_OUT");
+        return e ? atoi(e) : -1;
+    }();
+    if ((defer_env >= 0 ? defer_env != 0 : defer_outputs) && max_level > 2) {
+        std::vector<int> nread(n, 0);
+        for (size_t i = 0; i < n; i++)
+            if (live[i])
+                for (const auto &sv : ops[i].src)
+                    if (sv.ver >= 0) nread[sv.ver]++;
+        auto final_ver = [&](uint64_t key, int32_t ver) {
+            auto it = cur.find(key);
+            return ver < 0 ? it == cur.end() : (it != cur.end() && it->second == ver);
+        };
+        for (size_t i = 0; i < n; i++) {
+            if (!live[i] || nread[i] || rkind(ops[i].dst) == RK_U || ops[i].src.size() > 2) continue;
+            if (!final_ver(ops[i].dst, int32_t(i))) continue;
+            bool ok = true;
+            for (const auto &sv : ops[i].src) ok &= final_ver(sv.key, sv.ver);
+            if (ok) level[i] = max_level;
+        }
+    }
     auto plan = std::make_unique<Plan>();
     plan->tn = tn;
     plan->alpha = alpha;

@@ -107,6 +107,8 @@ class PlanBuilder {
     // >0: <= 2-source ops also substitute a still-read producer of <= dup_cost final
     // sources (CLAY_PLAN_DUP overrides); pairs with merge_slack
     int dup_cost = 0;
+    // move small final-output ops to the last level (CLAY_PLAN_DEFER_OUT overrides)
+    bool defer_outputs = false;
 
     // dst = XOR coef*src; terms on zero regions / zero coefs are dropped.
     void emit(uint64_t dst, const std::vector<std::pair<uint64_t, uint8_t>> &terms);
