@@ -1090,25 +1090,45 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
         ptrs.p[2 * pl.tn] = ws.ptr();
     }
     size_t launches = 0;
-    // consecutive 4 KiB tiles per block: 2 for deep plans (>= 4 levels: multi-erasure
-    // decodes, whose many small groups amortise their per-block scalar work over two
-    // tiles: (10,4,13) 4 erasures 1.026 -> 0.964 ms on one box), else 1 (4 and 8 measured
-    // slower everywhere; profiles/r02/gexec_tpw.txt).  CLAY_GEXEC_TPW overrides.
+    // Per-level block shape, from the level's block count at 4 KiB tiles (nwg = groups x
+    // tiles): tiny levels (nwg < CLAY_GEXEC_SMALL, default 2048 -- e.g. the 13-group tail
+    // level of a 4-erasure decode, latency-bound on ~1,300 blocks) run 1 KiB tiles (4-byte
+    // lanes) for 4x the blocks; large levels (nwg >= CLAY_GEXEC_BIG, default 32768: many
+    // small groups) give each block 2 consecutive tiles so a group's scalar work is
+    // amortised.  (10,4,13) 4-erasure decode 1.045 -> 0.968 ms same box; 1 KiB tiles on
+    // mid-size levels of wide groups cost 2x ((10,4,13) repair, 64 groups: 0.21 -> 0.40 ms),
+    // hence the low threshold (profiles/r02/gexec_block_shape.txt).  CLAY_GEXEC_TPW fixes
+    // the tiles per block for every level.
     static const int tpw_env = [] {
         const char *e = getenv("CLAY_GEXEC_TPW");
         const int v = e ? atoi(e) : 0;
         return v >= 1 && v <= 64 ? v : 0;
     }();
-    const uint32_t tpw = tpw_env ? uint32_t(tpw_env) : (pl.gstage_begin.size() >= 5 ? 2u : 1u);
-    const uint32_t tiles1 = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
-    const uint32_t tiles = (tiles1 + tpw - 1) / tpw;
+    static const uint64_t small_wg = [] {
+        const char *e = getenv("CLAY_GEXEC_SMALL");
+        return uint64_t(e ? atoll(e) : 2048);
+    }();
+    static const uint64_t big_wg = [] {
+        const char *e = getenv("CLAY_GEXEC_BIG");
+        return uint64_t(e ? atoll(e) : 32768);
+    }();
+    const uint32_t tiles16 = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
+    const uint32_t tiles4 = uint32_t((sc / 4 + 1 + kExecBlock - 1) / kExecBlock);
     for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
         uint32_t b = pl.gstage_begin[s], end = pl.gstage_begin[s + 1];
         const uint32_t maxd = pl.gstage_maxd[s];
+        const uint64_t nwg = uint64_t(end - b) * tiles16;
+        const bool narrow = !tpw_env && nwg < small_wg;
+        const uint32_t tpw = tpw_env ? uint32_t(tpw_env) : (nwg >= big_wg ? 2u : 1u);
+        const uint32_t tiles = narrow ? tiles4 : (tiles16 + tpw - 1) / tpw;
         while (b < end) {
             uint32_t n = std::min<uint32_t>(end - b, uint32_t(0x7fffffffu / tiles));
-            launch_gexec<16>(maxd, dim3(n * tiles), stream, ptrs, g, ds.d_tabs, b, tiles, sc, 0, sc, n, kBatchNone,
-                             nullptr, nullptr, 1, kExecBlock, tpw);
+            if (narrow)
+                launch_gexec<4>(maxd, dim3(n * tiles), stream, ptrs, g, ds.d_tabs, b, tiles, sc, 0, sc, n, kBatchNone,
+                                nullptr, nullptr, 1, kExecBlock, 1);
+            else
+                launch_gexec<16>(maxd, dim3(n * tiles), stream, ptrs, g, ds.d_tabs, b, tiles, sc, 0, sc, n,
+                                 kBatchNone, nullptr, nullptr, 1, kExecBlock, tpw);
             CLAY_HIP(hipGetLastError());
             launches++;
             b += n;
