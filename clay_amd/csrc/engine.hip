@@ -70,6 +70,12 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
                                                       uint8_t *const *__restrict__ ptab, uint32_t lps,
                                                       uint32_t nstripes, const ExecStride S, uint32_t tpw) {
     constexpr int NW = (VW + 3) / 4;
+    // perm tables of all 256 constants in LDS: a multiply's table is a broadcast LDS read,
+    // not a scalar-cache load whose address waits on the loaded coefficient
+    __shared__ __attribute__((aligned(16))) uint32_t ltab[256 * 8];
+    for (uint32_t i = threadIdx.x; i < 256u * 8u / 4u; i += kExecBlock)
+        reinterpret_cast<uint4 *>(ltab)[i] = reinterpret_cast<const uint4 *>(tabs)[i];
+    __syncthreads();
     // Block -> (group, tile).  order 0: group-major.  1: tile-major -- all groups of a
     // tile run back to back, so an input sub-chunk tile read by several groups is
     // re-read while still in L2 / MALL.  2: tile-major within contiguous per-XCD
@@ -156,7 +162,8 @@ __global__ __launch_bounds__(kExecBlock) void k_gexec(ExecPtrs P, const DevGroup
 #pragma unroll
                     for (int w = 0; w < NW; w++) acc[d][w] ^= v[b].w[w];
                 } else {
-                    const GfTab t = load_tab(tabs + c * 8);
+                    const uint4 t4 = *reinterpret_cast<const uint4 *>(ltab + c * 8u);
+                    const GfTab t{t4.x, t4.y, t4.z, t4.w, ltab[c * 8u + 4u]};
 #pragma unroll
                     for (int w = 0; w < NW; w++) acc[d][w] ^= gf_mul_idx(ix[w], t);
                 }
