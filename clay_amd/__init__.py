@@ -27,7 +27,7 @@ __all__ = [
     "ClayCode", "ClayError", "InvalidParameters", "InsufficientHelpers", "InvalidChunkSize",
     "InsufficientHelperData", "InconsistentChunkSizes", "TooManyErasures",
     "ReconstructionFailed", "MissingYSectionHelper", "Overflow", "DeviceError",
-    "set_encode_path", "last_encode_path", "last_launch_count",
+    "set_encode_path", "last_encode_path", "last_launch_count", "set_exec_mode", "last_exec_path",
 ]
 
 
@@ -119,6 +119,11 @@ def set_exec_mode(mode: str) -> str:
         raise ValueError(f"unknown exec mode {mode!r}")
     prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])
     return {v: k for k, v in _EXEC_MODES.items()}[prev]
+
+
+def last_exec_path() -> str:
+    """Plan executor of this thread's last decode / repair / staged encode: 'tile' | 'grouped'."""
+    return _lib.lib().clay_last_exec_path().decode()
 
 
 def release_workspace(device: int = 0) -> None:

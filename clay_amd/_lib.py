@@ -63,6 +63,7 @@ SIGNATURES = {
                                    _P(C.c_uint32), _sz, _P(C.c_uint32), _sz, _P(_sz), _err_p]),
     "clay_set_encode_path": (C.c_int, [C.c_int]),
     "clay_set_exec_mode": (C.c_int, [C.c_int]),
+    "clay_last_exec_path": (C.c_char_p, []),
     "clay_last_encode_path": (C.c_char_p, []),
     "clay_last_launch_count": (_sz, []),
     "clay_abi_version": (C.c_int, []),

@@ -536,6 +536,7 @@ __global__ __launch_bounds__(kFusedBlock) void k_fused_encode(FusedArgs a, const
 // synchronisation of a caller's stream.
 static thread_local std::string t_last_path = "none";
 static thread_local size_t t_last_launches = 0;
+static thread_local const char *t_last_exec = "none";  // plan executor of the last run_plan
 // Encode path selection (clay_set_encode_path): process-wide, read without locks.
 enum : int { kModeAuto = 0, kModeStaged = 1, kModeFused = 2, kModeBs = 3, kModeBs6 = 4, kModeStream = 5 };
 static std::atomic<int> g_encode_mode{kModeAuto};
@@ -1083,6 +1084,7 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
                          pl.gstage_begin.size() - 1, g.nu, maxd, vw);
         if (vw) {
             const uint32_t nst = uint32_t(pl.gstage_begin.size() - 1), ub = 2 * pl.tn;
+            t_last_exec = "tile";
             e = vw == 16 ? launch_texec<16>(maxd, ptrs, g, ds.d_tabs, nst, sc, ub, stream, dev)
               : vw == 8  ? launch_texec<8>(maxd, ptrs, g, ds.d_tabs, nst, sc, ub, stream, dev)
                          : launch_texec<4>(maxd, ptrs, g, ds.d_tabs, nst, sc, ub, stream, dev);
@@ -1097,6 +1099,7 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
         ptrs.p[2 * pl.tn] = ws.ptr();
     }
     size_t launches = 0;
+    t_last_exec = "grouped";
     // Per-level block shape, from the level's block count at 4 KiB tiles (nwg = groups x
     // tiles): tiny levels (nwg < CLAY_GEXEC_SMALL, default 2048 -- e.g. the 13-group tail
     // level of a 4-erasure decode, latency-bound on ~1,300 blocks) run 1 KiB tiles (4-byte
@@ -1958,6 +1961,7 @@ int clay_set_exec_mode(int mode) {
     return g_exec_mode.exchange(mode);
 }
 const char *clay_last_encode_path(void) { return t_last_path.c_str(); }
+const char *clay_last_exec_path(void) { return t_last_exec; }
 size_t clay_last_launch_count(void) { return t_last_launches; }
 
 int clay_new(size_t k, size_t m, size_t d, clay_code_t *out, clay_error_t *err) {

@@ -257,6 +257,9 @@ int clay_set_encode_path(int mode);
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
  * unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
+/* Plan executor the calling thread's last decode / repair / staged encode ran on:
+ * "tile" (k_texec), "grouped" (k_gexec) or "none". */
+const char *clay_last_exec_path(void);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
 const char *clay_last_encode_path(void);

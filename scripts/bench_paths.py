@@ -39,7 +39,7 @@ def report(name, ms, mn, algo, extra=None):
     d = {"config": name, "median_ms": round(ms, 4), "min_ms": round(mn, 4),
          "algorithmic_bytes": int(algo), "GBps": round(algo / (ms * 1e-3) / 1e9, 1),
          "frac_of_8TBps": round(algo / (ms * 1e-3) / 8e12, 4), "path": (clay_amd.last_encode_path() if name.startswith("encode")
-                  else ("tile" if clay_amd.last_launch_count() == 1 else "grouped")),
+                  else clay_amd.last_exec_path()),
          "launches": clay_amd.last_launch_count()}
     if extra:
         d.update(extra)

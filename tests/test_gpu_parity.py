@@ -210,11 +210,30 @@ def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
     try:
         got = c.repair(lost, pr, chunk)
         assert clay_amd.last_launch_count() == launches
+        # repair plans are one folded level: auto keeps them on the grouped executor
+        assert clay_amd.last_exec_path() == ("tile" if mode == "tile" else "grouped")
         clay_amd.set_exec_mode("grouped")
         assert c.repair(lost, pr, chunk) == got
     finally:
         clay_amd.set_exec_mode(prev)
     assert got == o.repair(lost, pr, chunk)
+
+
+@pytest.mark.parametrize("mode,expect", [("auto", "tile"), ("grouped", "grouped"), ("tile", "tile")])
+def test_small_decode_plan_executor(oracle_mod, mode, expect):
+    """(4,2,5) 1-erasure decode is a small two-level plan: auto runs it on the tile-fused
+    executor (one launch); every mode returns the oracle's bytes on random inputs."""
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    chunk = c.sub_chunk_no * (16 * 300 + 6)
+    chunks = np.random.default_rng(5).integers(0, 256, (c.n, chunk), dtype=np.uint8)
+    av = {i: chunks[i] for i in range(c.n) if i != 0}
+    prev = clay_amd.set_exec_mode(mode)
+    try:
+        got = c.decode(av, [0])
+        assert clay_amd.last_exec_path() == expect
+    finally:
+        clay_amd.set_exec_mode(prev)
+    assert got == o.decode(av, [0])
 
 
 def test_exec_mode_rejects_unknown():
