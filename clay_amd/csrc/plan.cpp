@@ -317,10 +317,19 @@ void Plan::group_ops() {
         const size_t slack = size_t(slack_env >= 0 ? slack_env : merge_slack);
         if (slack > 0 && gs.size() > 1) {
             std::vector<uint8_t> gone(gs.size(), 0);
+            // a group whose source list repeats a region (two versions of one slot) keeps
+            // its own rows: re-aligning by region would fold the two coefficients together
+            auto has_rep = [](const G &x) {
+                for (size_t j = 1; j < x.src.size(); j++)
+                    if (x.src[j] == x.src[j - 1]) return true;
+                return false;
+            };
             for (size_t a = 0; a < gs.size(); a++) {
-                if (gone[a] || gs[a].src.empty()) continue;
+                if (gone[a] || gs[a].src.empty() || has_rep(gs[a])) continue;
                 for (size_t b = a + 1; b < gs.size(); b++) {
-                    if (gone[b] || gs[b].src.empty() || gs[a].dst.size() + gs[b].dst.size() > kMaxGroupDst) continue;
+                    if (gone[b] || gs[b].src.empty() || gs[a].dst.size() + gs[b].dst.size() > kMaxGroupDst ||
+                        has_rep(gs[b]))
+                        continue;
                     std::vector<std::pair<uint32_t, uint32_t>> u;
                     std::set_union(gs[a].src.begin(), gs[a].src.end(), gs[b].src.begin(), gs[b].src.end(),
                                    std::back_inserter(u));
