@@ -63,6 +63,11 @@ def parse(argv=None):
     ap.add_argument("--path", default="auto",
                     choices=["auto", "fused", "staged", "bitsliced", "bitsliced6", "stream"])
     ap.add_argument("--tile", type=int, default=0, help="encode path variant (clay_set_encode_path)")
+    ap.add_argument("--launch-timeout", type=float, default=900.0,
+                    help="--gpus N launcher: stop every rank after this many seconds (0 = no limit)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="torch.distributed timeout (s) for init and collectives")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher tests
     ap.add_argument("--cpu-dry", action="store_true",
                     help="test mode without a GPU: the oracle replaces the device encode, gloo "
                          "replaces RCCL; everything else (launcher, ranks, timing, JSON) is the same")
@@ -80,6 +85,10 @@ def _free_port() -> int:
 
 
 def launch(args, argv) -> int:
+    """Spawn one rank process per GPU and supervise them: every rank is polled, and the
+    first rank that exits non-zero (bad ordinal, OOM, a fault) takes the others down at
+    once instead of leaving them blocked in a barrier -- the launcher then exits with that
+    rank's code.  The parent never touches HIP."""
     port = _free_port()
     procs = []
     for r in range(args.gpus):
@@ -89,10 +98,33 @@ def launch(args, argv) -> int:
                     "MASTER_PORT": str(port)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    deadline = time.monotonic() + args.launch_timeout if args.launch_timeout > 0 else None
     rc = 0
-    for p in procs:
-        r = p.wait()
-        rc = rc or r
+    live = set(range(len(procs)))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+        if rc != 0 or (deadline is not None and time.monotonic() > deadline):
+            if rc == 0:
+                rc = 124
+                print(f"bench: ranks still running after {args.launch_timeout:.0f} s; stopping them",
+                      file=sys.stderr, flush=True)
+            for r in live:
+                procs[r].terminate()
+            for r in live:
+                try:
+                    procs[r].wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    procs[r].kill()
+                    procs[r].wait()
+            break
+        time.sleep(0.05)
     return rc
 
 
@@ -269,10 +301,21 @@ def run_rank(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import datetime
+
     import torch
     import torch.distributed as dist
+    if rank == args.fail_rank:  # launcher test: this rank dies before the rendezvous
+        print(f"bench: rank {rank} failing on request (--fail-rank)", file=sys.stderr, flush=True)
+        return 3
+    if not args.cpu_dry:
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            print(f"bench: LOCAL_RANK {local} but only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
     if world > 1:
-        dist.init_process_group("gloo" if args.cpu_dry else "nccl")
+        dist.init_process_group("gloo" if args.cpu_dry else "nccl",
+                                timeout=datetime.timedelta(seconds=args.dist_timeout))
     from oracle import oracle  # checker / CPU legs only (and the dry run's stand-in encode)
     oracle.build()
 

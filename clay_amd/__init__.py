@@ -97,7 +97,8 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     """Process-wide encode path: 'auto' | 'staged' | 'fused' | 'bitsliced' | 'bitsliced6' | 'stream'.
 
     `tile` selects a variant: 'bitsliced' lanes per column group (0, 1, 4), 'bitsliced6'
-    tile width (0 = 256 B, 4 = 128 B), 'stream' loader waves (0 = default 2, 1, 2, 4).
+    tile width (0 = 256 B, 4 = 128 B), 'stream' loader waves for (10,4,13) (0 = default 4, 1, 2, 4;
+    (9,4,12) always runs 4). Only 'stream' and 'bitsliced6' need 8-byte rows (sc % 8 == 0).
     Every accepted path produces the reference's parity; anything else raises ValueError.
     Returns the previous path name."""
     if mode not in _ENCODE_PATHS:

@@ -592,8 +592,10 @@ struct Lease {
 struct PtrTable {
     void *d = nullptr;
     void *h = nullptr;  // pinned source of the upload, kept: a captured copy node reads it
+    hipEvent_t up = nullptr;  // recorded after the (eager) upload: other streams wait on it
     std::map<hipStream_t, hipEvent_t> evs;
     uint64_t last = 0;
+    int users = 0;  // calls between ptr_table() and ptr_table_done(): never freed meanwhile
     bool pinned = false;
 };
 constexpr size_t kMaxPtrTables = 64;
@@ -603,7 +605,8 @@ struct DevState {
     bool init = false;
     uint32_t *d_tabs = nullptr;                  // perm tables of all 256 constants
     std::vector<std::unique_ptr<Lease>> pool;    // workspaces and staging buffers
-    std::map<std::vector<uint8_t *>, PtrTable> tables;
+    std::map<std::vector<uint8_t *>, PtrTable> tables;       // eager uploads, shared by content
+    std::vector<std::unique_ptr<PtrTable>> captured;           // uploads inside a capture: graph-owned
     uint64_t tick = 0;
     std::vector<hipStream_t> host_streams;       // idle streams of the host-streaming pipeline
 };
@@ -757,43 +760,89 @@ struct LeaseGuard {
 };
 
 // Device copy of a batched launch's pointer table: uploaded once per distinct table
-// (hipMemcpyAsync from pinned memory on `st`), then reused by every call with the same
-// buffers -- no per-call synchronisation or blocking copy, and graph-capture safe.
+// (hipMemcpyAsync from pinned memory), then reused by every call with the same buffers --
+// no per-call synchronisation or blocking copy.
+//  * An eager upload records `up` on its stream; every later user waits on it
+//    (hipStreamWaitEvent), so a table first uploaded on stream A is never read on stream B
+//    before the copy has landed.
+//  * An upload inside a stream capture is only a graph node (it runs at replay), so it is
+//    never shared: each capture gets its own table, owned by the graph for good.
+//  * `users` counts calls between ptr_table() and ptr_table_done(); eviction and
+//    clay_release_workspace skip such tables, so a table is never freed between the lookup
+//    and the event that guards its last launch.
+static void free_table(PtrTable &t) {
+    for (auto &se : t.evs) {
+        (void)hipEventSynchronize(se.second);
+        (void)hipEventDestroy(se.second);
+    }
+    if (t.up) {
+        (void)hipEventSynchronize(t.up);
+        (void)hipEventDestroy(t.up);
+    }
+    (void)hipFree(t.d);
+    (void)hipHostFree(t.h);
+}
+static Error upload_table(PtrTable &t, const std::vector<uint8_t *> &tab, hipStream_t st, bool cap) {
+    const size_t bytes = tab.size() * sizeof(uint8_t *);
+    CLAY_HIP(hipMalloc(&t.d, bytes));
+    CLAY_HIP(hipHostMalloc(&t.h, bytes, hipHostMallocDefault));
+    std::memcpy(t.h, tab.data(), bytes);
+    CLAY_HIP(hipMemcpyAsync(t.d, t.h, bytes, hipMemcpyHostToDevice, st));
+    if (!cap) {
+        CLAY_HIP(hipEventCreateWithFlags(&t.up, hipEventDisableTiming));
+        CLAY_HIP(hipEventRecord(t.up, st));
+    }
+    return Error{};
+}
 static Error ptr_table(DevState &ds, const std::vector<uint8_t *> &tab, hipStream_t st, PtrTable **out) {
     std::lock_guard<std::mutex> lk(ds.mu);
+    if (capturing(st)) {
+        auto t = std::make_unique<PtrTable>();
+        t->pinned = true;
+        Error e = upload_table(*t, tab, st, true);
+        if (e) {
+            (void)hipFree(t->d);
+            (void)hipHostFree(t->h);
+            return e;
+        }
+        t->users = 1;
+        *out = t.get();
+        ds.captured.push_back(std::move(t));
+        return Error{};
+    }
     auto it = ds.tables.find(tab);
     if (it == ds.tables.end()) {
-        if (ds.tables.size() >= kMaxPtrTables) {  // evict the least recently used unpinned table
+        if (ds.tables.size() >= kMaxPtrTables) {  // evict the least recently used idle table
             auto victim = ds.tables.end();
             for (auto j = ds.tables.begin(); j != ds.tables.end(); ++j)
-                if (!j->second.pinned && (victim == ds.tables.end() || j->second.last < victim->second.last)) victim = j;
+                if (j->second.users == 0 && (victim == ds.tables.end() || j->second.last < victim->second.last))
+                    victim = j;
             if (victim != ds.tables.end()) {
-                for (auto &se : victim->second.evs) {
-                    (void)hipEventSynchronize(se.second);
-                    (void)hipEventDestroy(se.second);
-                }
-                (void)hipFree(victim->second.d);
-                (void)hipHostFree(victim->second.h);
+                free_table(victim->second);
                 ds.tables.erase(victim);
             }
         }
-        const size_t bytes = tab.size() * sizeof(uint8_t *);
         PtrTable t;
-        CLAY_HIP(hipMalloc(&t.d, bytes));
-        CLAY_HIP(hipHostMalloc(&t.h, bytes, hipHostMallocDefault));
-        std::memcpy(t.h, tab.data(), bytes);
-        CLAY_HIP(hipMemcpyAsync(t.d, t.h, bytes, hipMemcpyHostToDevice, st));
+        Error e = upload_table(t, tab, st, false);
+        if (e) {
+            free_table(t);
+            return e;
+        }
         it = ds.tables.emplace(tab, t).first;
+    } else if (it->second.up) {
+        CLAY_HIP(hipStreamWaitEvent(st, it->second.up, 0));  // the upload may be on another stream
     }
     it->second.last = ++ds.tick;
-    if (capturing(st)) it->second.pinned = true;
+    it->second.users++;
     *out = &it->second;
     return Error{};
 }
-// after the launches that read the table were enqueued on `st`
-static Error ptr_table_used(DevState &ds, PtrTable *t, hipStream_t st) {
+// After the launches that read the table were enqueued on `st` (or failed to be):
+// record the guard event and drop the caller's use.
+static Error ptr_table_done(DevState &ds, PtrTable *t, hipStream_t st, bool launched) {
     std::lock_guard<std::mutex> lk(ds.mu);
-    if (t->pinned) return Error{};
+    t->users--;
+    if (t->pinned || !launched) return Error{};
     auto it = t->evs.find(st);
     if (it == t->evs.end()) {
         hipEvent_t ev;
@@ -803,6 +852,21 @@ static Error ptr_table_used(DevState &ds, PtrTable *t, hipStream_t st) {
     CLAY_HIP(hipEventRecord(it->second, st));
     return Error{};
 }
+struct PtrTableUse {
+    DevState &ds;
+    hipStream_t st;
+    PtrTable *t = nullptr;
+    bool launched = false;
+    PtrTableUse(DevState &d, hipStream_t s) : ds(d), st(s) {}
+    Error done() {
+        PtrTable *x = t;
+        t = nullptr;
+        return x ? ptr_table_done(ds, x, st, launched) : Error{};
+    }
+    ~PtrTableUse() {
+        if (t) (void)ptr_table_done(ds, t, st, true);  // error path: guard whatever was enqueued
+    }
+};
 
 template <typename T>
 static Error upload_vec(const std::vector<T> &v, const T **out) {
@@ -903,6 +967,9 @@ static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::De
                 wbeg.push_back(uint32_t(terms.size()));
                 for (uint32_t gi = pl.gstage_begin[L] + w; gi < pl.gstage_begin[L + 1]; gi += nwv) {
                     const DevGroup &dg = pl.groups[gi];
+                    // a group without sources emits no term records, so k_texec would never
+                    // write its (zero) destinations: such plans run on k_gexec only
+                    if (dg.nsrc == 0 && dg.ndst > 0) g.nu = UINT32_MAX;
                     for (uint32_t j = 0; j < dg.nsrc; j++) {
                         const DevSrc &x = ts[dg.src_begin + j];
                         if (x.base > 255 || x.slot > 0xFFFFFFu || dg.dst_begin > 0xFFFFFFu || dg.ndst > 8)
@@ -1505,6 +1572,7 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
             P.p[2 * tn] = ws.ptr();
             S.s[2 * tn] = int64_t(tn * chunk);
         }
+        PtrTableUse ptu(ds, stream);
         PtrTable *pt = nullptr;
         if (!affine) {
             std::vector<uint8_t *> tab(ns * kMaxBases, nullptr);
@@ -1516,6 +1584,7 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
             }
             e = ptr_table(ds, tab, stream, &pt);
             if (e) return e;
+            ptu.t = pt;
         }
         for (size_t st = 0; st + 1 < pl.gstage_begin.size(); st++) {
             uint32_t b = pl.gstage_begin[st], end = pl.gstage_begin[st + 1];
@@ -1529,10 +1598,9 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
                 b += n;
             }
         }
-        if (pt) {
-            e = ptr_table_used(ds, pt, stream);
-            if (e) return e;
-        }
+        ptu.launched = true;
+        e = ptu.done();
+        if (e) return e;
     }
     t_last_launches += launches;
     t_last_path = "staged-batch";
@@ -1859,6 +1927,9 @@ static Error host_pipeline(int device, size_t sc, const std::vector<HostIn> &ins
         std::vector<hipStream_t> st;
         std::vector<Lease *> buf;
         ~Res() {
+            // every exit path, errors included: copies to / from the caller's host buffers
+            // may still be queued, and the caller may free those buffers once we return
+            for (auto x : st) (void)hipStreamSynchronize(x);
             for (size_t i = 0; i < buf.size(); i++) lease_release(ds, buf[i], st[i]);
             std::lock_guard<std::mutex> lk(ds.mu);
             for (auto x : st) ds.host_streams.push_back(x);
@@ -2124,16 +2195,11 @@ int clay_release_workspace(int device, clay_error_t *err) {
         }
     }
     for (auto it = ds->tables.begin(); it != ds->tables.end();) {
-        if (it->second.pinned) {
+        if (it->second.users > 0) {  // a call between lookup and launch holds it
             ++it;
             continue;
         }
-        for (auto &se : it->second.evs) {
-            (void)hipEventSynchronize(se.second);
-            (void)hipEventDestroy(se.second);
-        }
-        (void)hipFree(it->second.d);
-        (void)hipHostFree(it->second.h);
+        free_table(it->second);
         it = ds->tables.erase(it);
     }
     return 0;

@@ -232,8 +232,9 @@ size_t clay_workspace_bytes(int device);
  *                  compiled instantiation; else the byte-sliced fused kernel when the
  *                  parity is one y-section; else the staged plan executor.  Batches of
  *                  >= 4 stripes of <= 4 MiB of data run as one staged launch per level.
- *                  Bit-sliced kernels need sub-chunks that are multiples of 8 bytes
- *                  and 8-byte aligned chunk pointers.
+ *                  The LDS-DMA kernels (stream, bitsliced6) need sub-chunks that are
+ *                  multiples of 8 bytes and 8-byte aligned chunk pointers (else auto
+ *                  falls through); the v1 kernel takes any sub-chunk size and alignment.
  *   1 staged    -- the plan executor (k_gexec), any code
  *   2 fused     -- byte-sliced fused kernel (q == m <= 4)
  *   3 bitsliced -- bit-sliced v1 (register loads); variant = lanes per column group
@@ -241,7 +242,8 @@ size_t clay_workspace_bytes(int device);
  *   4 bitsliced6-- v6 (column-per-lane, 2-slot LDS ring), (10,4,13); variant 0 = 256-B
  *                  tiles, 4 = 128-B tiles
  *   5 stream    -- the streaming kernel (stream_encode.hpp); variant = loader waves
- *                  0 (= 2), 1, 2, 4
+ *                  for (10,4,13): 0 (= 4, the default), 1, 2, 4; (9,4,12) always runs
+ *                  4 loader waves (its variant is accepted and ignored)
  * Bits 8..15 = variant.  Every accepted (path, variant) produces the reference's
  * parity bytes; any other value returns -1 and leaves the setting unchanged.
  * Returns the previous setting (path | variant << 8). */

@@ -45,3 +45,38 @@ def test_bench_launcher_cpu_dry(oracle_mod, world):
     for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "vs_baseline", "dtype",
                 "data", "config", "roofline"):
         assert key in d
+
+
+def test_bench_launcher_rank_failure_stops_job(oracle_mod):
+    """A rank that dies before the rendezvous (bad ordinal, OOM ...) must not leave the
+    other rank blocked in init / barrier: the launcher sees the first non-zero exit,
+    terminates the rest and exits non-zero, well within 60 s."""
+    import time
+    stripe = 10 * 256 * 2 * 64
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-dry",
+                        "--stripe-bytes", str(stripe), "--steps", "3", "--warmup", "1", "--cpu-seconds", "0",
+                        "--fail-rank", "1"], capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    el = time.monotonic() - t0
+    assert r.returncode != 0
+    assert "rank 1 exited with 3" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert el < 60, el
+
+
+def test_bench_rank_rejects_missing_device():
+    """A rank whose LOCAL_RANK has no GPU fails fast with a clear message (here: no GPU at
+    all in the container, LOCAL_RANK 0)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update({"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 2
+    assert "only 0 GPU(s) visible" in r.stderr

@@ -219,6 +219,79 @@ def test_batch_encode_non_affine_pointers(oracle_mod, torch_cuda, sc, n):
             assert np.array_equal(got[slot[s] * m:(slot[s] + 1) * m], refs[s][k:]), s
 
 
+def test_non_affine_table_across_streams_and_capture(oracle_mod, torch_cuda):
+    """A non-affine pointer table first uploaded on stream A is then used on stream B
+    (which must wait for A's upload), inside a graph capture on stream C (a private,
+    graph-owned upload), and eagerly again after the capture -- every result bit-exact.
+    Outputs start as 0xFF so a skipped write shows."""
+    torch = torch_cuda
+    k, m, d = 6, 3, 8
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    n, sc = 40, 32
+    chunk = c.sub_chunk_no * sc
+    refs = [_stripe(o, k, chunk, 1300 + s) for s in range(n)]
+    perm = np.random.default_rng(5).permutation(n)
+    data = torch.from_numpy(np.concatenate([refs[s][:k] for s in perm])).cuda()
+    slot = {s: j for j, s in enumerate(perm)}
+    pars = [torch.full((n * m, chunk), 0xFF, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    dl = [data[slot[s] * k + i] for s in range(n) for i in range(k)]
+
+    def pl(par):
+        return [par[slot[s] * m + i] for s in range(n) for i in range(m)]
+
+    def check(par, what):
+        got = par.cpu().numpy()
+        for s in range(n):
+            assert np.array_equal(got[slot[s] * m:(slot[s] + 1) * m], refs[s][k:]), (what, s)
+
+    clay_amd.release_workspace(0)
+    sa, sb, sc_, sd = (torch.cuda.Stream() for _ in range(4))
+    # A uploads the table for pars[0]'s pointer set; B reuses the same set right away
+    c.encode_device_batch(dl, pl(pars[0]), n, chunk, 0, sa.cuda_stream)
+    c.encode_device_batch(dl, pl(pars[0]), n, chunk, 0, sb.cuda_stream)
+    sb.synchronize()
+    sa.synchronize()
+    check(pars[0], "A then B")
+    # a table first seen inside a capture, then the same pointer set eagerly on D
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=sc_):
+        c.encode_device_batch(dl, pl(pars[1]), n, chunk, 0, torch.cuda.current_stream().cuda_stream)
+    c.encode_device_batch(dl, pl(pars[1]), n, chunk, 0, sd.cuda_stream)
+    sd.synchronize()
+    check(pars[1], "eager after capture")
+    pars[1].fill_(0xFF)
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    check(pars[1], "replay")
+
+
+def test_tile_executor_writes_every_output(oracle_mod, torch_cuda):
+    """Decode and repair under the tile-fused executor with outputs pre-filled with 0xFF:
+    every destination byte is written (no stale caller bytes survive)."""
+    torch = torch_cuda
+    prev = clay_amd.set_exec_mode("tile")
+    try:
+        for (k, m, d), er, lost in (((4, 2, 5), [0], 1), ((6, 3, 8), [1, 7], 0)):
+            c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+            n = k + m
+            chunk = c.sub_chunk_no * 1024
+            ref = _stripe(o, k, chunk, 77 + k)
+            full = torch.from_numpy(ref).cuda()
+            outs = torch.full((n, chunk), 0xFF, dtype=torch.uint8, device="cuda")
+            c.decode_device([None if j in er else full[j] for j in range(n)], er,
+                            [outs[j] if j in er else None for j in range(n)], chunk)
+            rep = torch.full((chunk,), 0xFF, dtype=torch.uint8, device="cuda")
+            info = c.minimum_to_repair(lost, [i for i in range(n) if i != lost])
+            c.repair_device_full_chunks(lost, [h for h, _ in info], [full[h] for h, _ in info], chunk, rep)
+            torch.cuda.synchronize()
+            for e in er:
+                assert np.array_equal(outs[e].cpu().numpy(), ref[e]), ((k, m, d), e)
+            assert np.array_equal(rep.cpu().numpy(), ref[lost]), ((k, m, d), "repair")
+    finally:
+        clay_amd.set_exec_mode(prev)
+
+
 @pytest.mark.parametrize("cfg,sc,n,pad", [((4, 2, 5), 32, 300, 0), ((4, 2, 5), 32, 3, 0), ((10, 4, 13), 40, 9, 64),
                                           ((9, 3, 11), 2, 257, 16), ((6, 3, 8), 4104, 5, 0),
                                           ((10, 4, 13), 2048, 5, 0)])
