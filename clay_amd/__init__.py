@@ -109,13 +109,14 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
-_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2}
+_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3}
 
 
 def set_exec_mode(mode: str) -> str:
     """Process-wide plan executor for decode / repair / staged encode: 'auto' (tile-fused
     where the U slots fit in LDS, else grouped), 'grouped' (one launch per level) or
-    'tile'.  Every mode produces the reference's bytes.  Returns the previous mode."""
+    'tile', or 'stream' (the single-launch streaming decode for q = 4, t = 4 codes where
+    eligible, else as auto).  Every mode produces the reference's bytes.  Returns the previous mode."""
     if mode not in _EXEC_MODES:
         raise ValueError(f"unknown exec mode {mode!r}")
     prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])

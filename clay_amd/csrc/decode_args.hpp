@@ -1,0 +1,37 @@
+// decode_args.hpp -- kernel arguments of the streaming decode (stream_decode.hpp), shared by
+// the host planner (engine.hip) and the kernel translation unit (decode_stream.hip).
+#pragma once
+#include <stdint.h>
+
+namespace clay {
+namespace bs {
+
+constexpr int kDecBuf = 16384;  // one LDS node buffer: 256 layers x 64 B
+
+struct DecArgs {
+    const uint8_t *node[16];  // internal nodes with data (alive real nodes), else nullptr
+    uint8_t *out[4];          // per erased index r: output chunk (nullptr: not wanted)
+    uint64_t sc;
+    uint32_t region, nslots;  // XCD region bytes (multiple of 64), workgroups per XCD
+    uint32_t alive;           // bit i: internal node i has data
+    uint32_t used;            // bit i: node i is among the first 12 present (the RS rows used)
+    uint32_t ne;              // erased count (1..4)
+    int32_t rix[16];          // erased index r of internal node i, else -1
+    uint32_t emask[4];        // per section y: bit x set if node (y, x) is erased
+    uint32_t ring;            // staging ring buffers R = 10 - ne
+    uint32_t nt;              // loads per tile (alive nodes)
+    uint32_t sec_off[5];      // first load of section y's step within a tile
+    uint32_t load_node[16];   // internal node of each load of a tile
+    uint32_t nround;          // phase-B rounds
+    uint32_t round_start[24]; // first entry of each round in the layer order (+ end)
+    // device buffer (kDecTabWords dwords), copied into LDS for phase B: v_perm tables of 8
+    // dwords each (5 used) -- table t = r * 4 + j: row e_r of H_K^-1, check j; table
+    // 16 + i * 4 + r: A_i[e_r] = (H_K^-1 gamma H_i)[e_r] for node i; then the phase-B layer
+    // order (256 bytes) at dword kDecOrder
+    const uint32_t *tabs;
+};
+constexpr int kDecOrder = 640;
+constexpr int kDecTabWords = 768;  // 3 KiB: three 1 KiB LDS-DMA instructions
+
+}  // namespace bs
+}  // namespace clay

@@ -33,6 +33,7 @@
 #include "bitslice.hpp"
 #include "bitslice6.hpp"
 #include "stream_encode.hpp"
+#include "decode_args.hpp"  // streaming-decode kernel: stream_decode.hpp, instantiated in decode_stream.hip
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -599,6 +600,7 @@ struct PtrTable {
     bool pinned = false;
 };
 constexpr size_t kMaxPtrTables = 64;
+constexpr size_t kCapArena = size_t(4) << 20;  // pointer tables created inside stream captures
 
 struct DevState {
     std::mutex mu;  // everything below
@@ -606,7 +608,11 @@ struct DevState {
     uint32_t *d_tabs = nullptr;                  // perm tables of all 256 constants
     std::vector<std::unique_ptr<Lease>> pool;    // workspaces and staging buffers
     std::map<std::vector<uint8_t *>, PtrTable> tables;       // eager uploads, shared by content
-    std::vector<std::unique_ptr<PtrTable>> captured;           // uploads inside a capture: graph-owned
+    // tables of calls inside a stream capture: bump-allocated from this arena (no hipMalloc
+    // while capturing), owned by the captured graphs for good
+    uint8_t *cap_d = nullptr, *cap_h = nullptr;
+    size_t cap_used = 0;
+    std::vector<std::unique_ptr<PtrTable>> captured;
     uint64_t tick = 0;
     std::vector<hipStream_t> host_streams;       // idle streams of the host-streaming pipeline
 };
@@ -631,6 +637,7 @@ struct CodeState {
     };
     std::map<std::pair<const Plan *, int>, DevGrouped> gplan;
     std::map<int, uint32_t *> mtab;
+    std::map<std::pair<std::vector<uint32_t>, int>, const uint32_t *> dtabs;  // stream-decode tables
     explicit CodeState(const clay_code_t &c) : code(c), rs(c) {}
 };
 static std::mutex g_codes_mu;
@@ -673,6 +680,8 @@ static Error dev_state(int dev, DevState **out) {
         for (int c = 0; c < 256; c++) perm_table(uint8_t(c), &tabs[c * 8]);
         CLAY_HIP(hipMalloc(&s.d_tabs, tabs.size() * 4));
         CLAY_HIP(hipMemcpy(s.d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+        CLAY_HIP(hipMalloc(&s.cap_d, kCapArena));
+        CLAY_HIP(hipHostMalloc(&s.cap_h, kCapArena, hipHostMallocDefault));
         s.init = true;
     }
     *out = &s;
@@ -797,14 +806,18 @@ static Error upload_table(PtrTable &t, const std::vector<uint8_t *> &tab, hipStr
 static Error ptr_table(DevState &ds, const std::vector<uint8_t *> &tab, hipStream_t st, PtrTable **out) {
     std::lock_guard<std::mutex> lk(ds.mu);
     if (capturing(st)) {
+        // no allocation and no cross-capture event while capturing: a private copy from the
+        // arena, uploaded by the graph's own copy node at every replay
+        const size_t bytes = (tab.size() * sizeof(uint8_t *) + 255) / 256 * 256;
+        if (ds.cap_used + bytes > kCapArena)
+            return make_error(CLAY_ERR_DEVICE, ds.cap_used, bytes, 0, "pointer-table arena for captured calls exhausted");
         auto t = std::make_unique<PtrTable>();
         t->pinned = true;
-        Error e = upload_table(*t, tab, st, true);
-        if (e) {
-            (void)hipFree(t->d);
-            (void)hipHostFree(t->h);
-            return e;
-        }
+        t->d = ds.cap_d + ds.cap_used;
+        t->h = ds.cap_h + ds.cap_used;
+        ds.cap_used += bytes;
+        std::memcpy(t->h, tab.data(), tab.size() * sizeof(uint8_t *));
+        CLAY_HIP(hipMemcpyAsync(t->d, t->h, tab.size() * sizeof(uint8_t *), hipMemcpyHostToDevice, st));
         t->users = 1;
         *out = t.get();
         ds.captured.push_back(std::move(t));
@@ -1072,7 +1085,7 @@ static int align_of(uintptr_t p) {
 }
 
 // Executor selection (clay_set_exec_mode): process-wide, read without locks.
-enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2 };
+enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3 };  // see clay_set_exec_mode
 static std::atomic<int> g_exec_mode{kExecAuto};
 static size_t tex_lds_budget() {
     static const size_t b = [] {
@@ -1140,7 +1153,7 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     // 0.038 ms.  On the big plans it measured slower than the grouped executor ((9,3,11)
     // repair 0.53 vs 0.43 ms, (10,4,13) 1-erasure decode 0.72 vs 0.41 ms),
     // so "tile" mode runs it wherever eligible but auto does not.
-    const bool tex_ok = xm == kExecTile || (xm == kExecAuto && pl.groups.size() <= kTexAutoGroups &&
+    const bool tex_ok = xm == kExecTile || ((xm == kExecAuto || xm == kExecStream) && pl.groups.size() <= kTexAutoGroups &&
                                              pl.gstage_begin.size() > 2);  // one level: nothing to fuse
     if (tex_ok && sc > 0 && sc / (64 * 4) < 0x7fffffffu) {
         uint32_t maxd = 1;
@@ -1750,6 +1763,145 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
 // ---------------------------------------------------------------------------
 // Decode / repair on device
 // ---------------------------------------------------------------------------
+// The single-launch streaming decode (stream_decode.hpp) for q = 4, t = 4 codes with
+// k = 9 / 10: any erasure pattern of <= 4 nodes with at most one erasure per y-section (two
+// erasures in one section need a PFT pair between items of the same round: those patterns stay
+// on the plan executor).  `cin` / `cout`: internal node pointers (inputs of present nodes,
+// outputs of erased nodes, nullptr if not wanted).
+hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
+
+template <int KD>
+static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
+                                  const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream, bool *done) {
+    *done = false;
+    const clay_code_t &c = cs.code;
+    using S = bs::Shape<KD, 4>;
+    if (int(c.k) != KD || c.m != 4 || c.q != 4 || c.t != 4 || c.q * c.t != 16) return Error{};
+    if (sc % 8 || sc < 512 || double(S::ALPHA) * double(sc) >= 4294967296.0) return Error{};
+    const GF &gf = GF::get();
+    std::vector<int> E;
+    int per_sec[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; i++)
+        if (erased[i]) {
+            E.push_back(i);
+            per_sec[i / 4]++;
+        }
+    if (E.empty() || E.size() > 4) return Error{};
+    for (int y = 0; y < 4; y++)
+        if (per_sec[y] > 1) return Error{};  // PFT pair inside a round: not in this kernel
+    for (int i = 0; i < 16; i++) {
+        if (cin[i] && reinterpret_cast<uintptr_t>(cin[i]) % 8) return Error{};
+        if (cout[i] && reinterpret_cast<uintptr_t>(cout[i]) % 8) return Error{};
+    }
+    for (int p = 0; p < 4; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    bs::DecArgs a{};
+    // RS rows used: the first 12 present shards (reconstruct, decode.rs:374); K = the rest
+    uint32_t used = 0;
+    int nused = 0;
+    std::vector<int> Kset;
+    for (int i = 0; i < 16; i++) {
+        if (!erased[i] && nused < S::K) {
+            used |= 1u << i;
+            nused++;
+        } else {
+            Kset.push_back(i);
+        }
+    }
+    if (nused != S::K || Kset.size() != 4) return Error{};
+    auto Hc = [&](int pchk, int i) -> uint8_t {
+        return i < S::K ? cs.rs.gen[(S::K + pchk) * S::K + i] : uint8_t(i - S::K == pchk ? 1 : 0);
+    };
+    std::vector<uint8_t> hk(16), hinv;
+    for (int pchk = 0; pchk < 4; pchk++)
+        for (int j = 0; j < 4; j++) hk[pchk * 4 + j] = Hc(pchk, Kset[j]);
+    if (!gf_invert(hk, 4, hinv)) return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "singular RS check submatrix");
+    a.ne = uint32_t(E.size());
+    std::vector<uint32_t> tabs(bs::kDecTabWords, 0);
+    for (int i = 0; i < 16; i++) a.rix[i] = -1;
+    for (size_t r = 0; r < E.size(); r++) {
+        const int e = E[r];
+        a.rix[e] = int(r);
+        a.emask[e / 4] |= 1u << (e % 4);
+        a.out[r] = cout[e];
+        const int row = int(std::find(Kset.begin(), Kset.end(), e) - Kset.begin());
+        for (int j = 0; j < 4; j++) perm_table(hinv[row * 4 + j], &tabs[(r * 4 + j) * 8]);
+        for (int i = 0; i < 16; i++) {  // A_(y,x)[e_r] = (H_K^-1 gamma H_i)[row of e_r], i = 4y + x
+            uint8_t v = 0;
+            for (int j = 0; j < 4; j++) v ^= gf.mul(hinv[row * 4 + j], gf.mul(kGamma, Hc(j, i)));
+            perm_table(v, &tabs[(16 + i * 4 + r) * 8]);
+        }
+    }
+    a.used = used;
+    const uint32_t R = 10 - a.ne;
+    uint32_t n[4] = {0, 0, 0, 0}, nt = 0;
+    for (int y = 0; y < 4; y++) {
+        a.sec_off[y] = nt;
+        for (int x = 0; x < 4; x++) {
+            const int i = 4 * y + x;
+            a.node[i] = cin[i];
+            if (cin[i]) {
+                a.alive |= 1u << i;
+                a.load_node[nt++] = uint32_t(i);
+                n[y]++;
+            }
+        }
+    }
+    a.sec_off[4] = nt;
+    a.nt = nt;
+    if (nt == 0) return Error{};
+    for (int y = 0; y < 4; y++)
+        if (n[y] > R || (y < 3 && n[y] + n[y + 1] > R)) return Error{};
+    if (R < 5) return Error{};  // S/C region (4 buffers) + the phase-B table buffer
+    a.ring = R;
+    // phase-B layer order: by iscore level (red erased sections), then by the set of red
+    // sections (uniform corrections per wave), rounds of <= 64 layers of one level
+    std::vector<std::pair<uint32_t, int>> lay;
+    for (int z = 0; z < 256; z++) {
+        uint32_t red = 0;
+        for (int y = 0; y < 4; y++)
+            if ((a.emask[y] >> ((z >> (2 * (3 - y))) & 3)) & 1u) red |= 1u << y;
+        lay.push_back({uint32_t(__builtin_popcount(red)) << 8 | red, z});
+    }
+    std::stable_sort(lay.begin(), lay.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    uint8_t *ord = reinterpret_cast<uint8_t *>(&tabs[bs::kDecOrder]);
+    uint32_t nr = 0;
+    for (size_t i = 0; i < lay.size(); i++) {
+        ord[i] = uint8_t(lay[i].second);
+        const bool new_level = i == 0 || (lay[i].first >> 8) != (lay[i - 1].first >> 8);
+        if (new_level || i - a.round_start[nr - 1] >= 64) {
+            if (nr + 1 >= sizeof(a.round_start) / sizeof(a.round_start[0])) return Error{};
+            a.round_start[nr++] = uint32_t(i);
+        }
+    }
+    a.round_start[nr] = 256;
+    a.nround = nr;
+    a.sc = sc;
+    a.region = uint32_t(((sc + 7) / 8 + 63) / 64 * 64);
+    const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
+    a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
+    // the pattern's tables: uploaded once per (pattern, device), cached with the code
+    {
+        std::lock_guard<std::mutex> lk(cs.mu);
+        auto key = std::make_pair(std::vector<uint32_t>(tabs), prop.dev);
+        auto it = cs.dtabs.find(key);
+        if (it == cs.dtabs.end()) {
+            const uint32_t *d = nullptr;
+            Error ue = upload_vec(tabs, &d);
+            if (ue) return ue;
+            it = cs.dtabs.emplace(key, d).first;
+        }
+        a.tabs = it->second;
+    }
+    CLAY_HIP(launch_stream_decode_kernel(KD, a, stream, prop.dev));
+    t_last_launches++;
+    t_last_exec = "stream";
+    *done = true;
+    return Error{};
+}
+
 static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
                                 uint8_t *const *outs, size_t chunk, int dev, void *stream) {
     Error e = check_code(code);
@@ -1794,6 +1946,21 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     for (size_t i = 0; i < c.n; i++) {
         size_t in = internal_of(c, i);
         P.p[in] = chunks[i] ? const_cast<uint8_t *>(chunks[i]) : (want[in] ? outs[i] : nullptr);
+    }
+    if (g_exec_mode.load(std::memory_order_relaxed) == kExecStream && tn == 16) {
+        const uint8_t *cin[16] = {};
+        uint8_t *cout[16] = {};
+        for (size_t i = 0; i < c.n; i++) {
+            const size_t in = internal_of(c, i);
+            if (erased[in]) cout[in] = want[in] ? outs[i] : nullptr;
+            else cin[in] = chunks[i];
+        }
+        bool done = false;
+        const DevProps &prop = dev_props(dev);
+        const size_t sc = chunk / c.sub_chunk_no;
+        if (c.k == 10) e = launch_stream_decode<10>(cs, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
+        else if (c.k == 9) e = launch_stream_decode<9>(cs, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
+        if (e || done) return e;
     }
     return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
 }
@@ -2028,7 +2195,7 @@ int clay_set_encode_path(int mode) {
     return prev;
 }
 int clay_set_exec_mode(int mode) {
-    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile) return -1;
+    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream) return -1;
     return g_exec_mode.exchange(mode);
 }
 const char *clay_last_encode_path(void) { return t_last_path.c_str(); }

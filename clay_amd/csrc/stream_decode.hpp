@@ -1,0 +1,460 @@
+// stream_decode.hpp -- single-launch decode for codes with q = 4, t = 4 (alpha = 256), e.g. the
+// BASELINE (10,4,13) with up to 4 erasures: every survivor byte is read from HBM once, every
+// output byte written once, and all iscore rounds of the reference's layered decode
+// (decode.rs:196-254) run inside the workgroup.
+//
+// Algebra (syndrome form of decode_layered / decode_uncoupled_layer, decode.rs:260-408).
+// Per layer z the RS step sees the 16 uncoupled values U(i, z); H = [G | I] is the 4 x 16
+// parity-check matrix of the RS(12,4) generator (G = its parity rows, compile time).  The
+// reference reconstructs from the first 12 present shards ("used" set; reed-solomon-erasure
+// 6.0.0 reconstruct) -- the unique codeword through them -- so with K = the 4 other nodes
+// (erased + ignored) U_K(z) = H_K^-1 * S(z), S(z) = sum_{i used} H_i U(i, z), bit for bit even on
+// inputs that are not codewords.  U(i, z) of a used node is its PRT value (transforms.rs:42-55);
+// where its companion is erased the term gamma * C(e, z') is unknown until the lower-iscore layer
+// z' is solved, so:
+//   phase A (streaming): S_known(z) = sum_i H_i U'(i, z) with those terms dropped, and
+//            Out(e, z) = gamma * C(companion of e at z) for erased e (compute_c_from_u_and_cstar)
+//   phase B (rounds in iscore order): U_e(z) = row e of H_K^-1 S_known(z)
+//            + sum over the dropped terms A_(y,x)[e] C(e_y, z[y:=x])  (A = H_K^-1 gamma H_(y,x)),
+//            C(e, z) = U_e(z) + Out(e, z)  (Out = 0 where e is red).
+//
+// Phase A tile and lane map.  A workgroup owns W = 64 byte positions of every (node, layer) row.
+// Section G (template, 3) is the lane's "slot" digit: lane (column c = the other three digits,
+// part p) owns the four layers (c, g = 0..3) x 8 positions = 32 symbols = one bit-sliced dword
+// per plane, so section G's PRT pairs stay inside the lane and the other sections' companions
+// are read from LDS.  Node buffer (LDS, 16 KiB) = one node x 256 layers x 64 B; row (c, g) at
+// c * 256 + (g ^ (c & 3)) * 64 (own and companion ds_read_b64 bank-conflict free; one 1 KiB
+// LDS-DMA instruction = 4 columns = 16 whole 64-B row runs).  One step per section: its alive
+// nodes stream through a ring of node buffers filled by 4 dedicated loader waves.
+//
+// Phase B: S_known goes to LDS; each round gives every lane ONE item (layer z, part p: 8
+// positions) of one iscore level, layers sorted on the host by (level, set of red sections) so a
+// wave's corrections are uniform.  A round only reads C of earlier rounds; C overwrites the
+// item's own S slots.  The iscore dependency therefore costs a few short rounds instead of
+// divergent passes over every lane.
+//
+// LDS (10 x 16 KiB): ring of R = 10 - ne node buffers; Out(e, ., .) in the top ne buffers; during
+// phase B the S/C region (4 x 16 KiB, [j][z][p] x 8 B) reuses ring buffers R-4 .. R-1 while the
+// loaders prefetch the next tile's first nodes into buffers 0 .. R-5.
+#pragma once
+
+#include "decode_args.hpp"
+#include "kernels.hpp"
+#include "stream_encode.hpp"  // uniform_ptr, bit-slice helpers
+
+namespace clay {
+namespace bs {
+
+
+
+// tables read through the constant address space: uniform-address loads become s_load
+typedef const __attribute__((address_space(4))) uint32_t *cu32p;
+__device__ __forceinline__ GfTab load_tab_c(cu32p t) {
+    GfTab r;
+    r.w0 = t[0];
+    r.w1 = t[1];
+    r.w2 = t[2];
+    r.w3 = t[3];
+    r.w4 = t[4];
+    return r;
+}
+
+// an opaque copy of a per-lane value: everything derived from it is recomputed where it is
+// used instead of being hoisted out of the tile loop into long-lived (spilled) registers
+__device__ __forceinline__ uint32_t opq(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+template <int KD, int G>
+struct StreamDec {
+    using S = Shape<KD, 4>;
+    static_assert(S::Q == 4 && S::T == 4 && S::K == 12, "q = 4, t = 4, 12 RS data rows");
+    static constexpr int W = 64, CWAVES = 8, LOADERS = 4, BLOCK = 64 * (CWAVES + LOADERS);
+    static constexpr int BUF = 16384;                // one node: 256 layers x 64 B
+    static constexpr int LDS_BYTES = 10 * BUF;       // ring + exchange buffers
+    static constexpr int BPL = 16 / LOADERS;         // 1 KiB blocks per node buffer per loader wave
+
+    // H = [G | I]: check p, internal node i
+    static constexpr uint8_t H(int p, int i) { return i < S::K ? S::RS.g[p][i] : uint8_t(i - S::K == p ? 1 : 0); }
+    static constexpr int cd(int k) { return k < G ? k : k + 1; }  // column digit k -> section
+    static constexpr int ck(int y) { return y < G ? y : y - 1; }  // section (!= G) -> column digit
+    static constexpr int csh(int y) { return 2 * (2 - ck(y)); }   // shift of section y's digit in c
+    static constexpr uint32_t wt(int y) { return 1u << (2 * (3 - y)); }  // layer weight 4^(3-y)
+
+    __host__ __device__ static uint32_t layer0(uint32_t c) {
+        uint32_t z = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) z += ((c >> (2 * (2 - k))) & 3u) * wt(cd(k));
+        return z;
+    }
+    // byte offset of row (c, g) within a node buffer
+    __device__ static uint32_t row(uint32_t c, uint32_t g) { return c * 256u + ((g ^ (c & 3u)) << 6); }
+
+    // 8 dwords = the lane's 4 slots x 8 positions of one node at column cc
+    __device__ static void read4(const uint8_t *buf, uint32_t cc, uint32_t poff, uint32_t (&d)[8]) {
+        const uint32_t b = cc * 256u + poff, cl = cc & 3u;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(buf + (b + ((uint32_t(g) ^ cl) << 6)));
+            d[2 * g] = v.x;
+            d[2 * g + 1] = v.y;
+        }
+    }
+    __device__ static void write4(uint8_t *buf, uint32_t cc, uint32_t poff, const uint32_t (&d)[8]) {
+        const uint32_t b = cc * 256u + poff, cl = cc & 3u;
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+            *reinterpret_cast<uint2 *>(buf + (b + ((uint32_t(g) ^ cl) << 6))) = make_uint2(d[2 * g], d[2 * g + 1]);
+    }
+
+    // S[p] (8 planes) ^= f * H(p, I) * u, f = gamma if GAMMA
+    template <int I, bool GAMMA>
+    __device__ static void fold(const uint32_t (&u)[8], uint32_t (&s)[32]) {
+        sfor<4>([&](auto pc) BS_INL {
+            constexpr int p = decltype(pc)::value;
+            constexpr uint8_t h = GAMMA ? gm(2, H(p, I)) : H(p, I);
+            if constexpr (h != 0) {
+                sfor<8>([&](auto bc) BS_INL {
+                    constexpr int bo = decltype(bc)::value;
+                    constexpr uint64_t mk = plane_mask(h, bo, 0);
+                    s[p * 8 + bo] = xor_sel<mk, true>(s[p * 8 + bo], u);
+                });
+            }
+        });
+    }
+
+    // ---------------- tile map ----------------
+    struct Tile {
+        uint32_t b0, vend;
+    };
+    struct Map {
+        uint32_t x0, x1, n;
+        __device__ Map(uint32_t sc, uint32_t region, uint32_t ns, uint32_t xcd, uint32_t slot) {
+            x0 = xcd * region;
+            x1 = x0 + region < sc ? x0 + region : sc;
+            n = 0;
+            if (x0 < x1) {
+                const uint32_t nt = (x1 - x0 + uint32_t(W) - 1) / uint32_t(W);
+                n = nt > slot ? (nt - slot + ns - 1) / ns : 0;
+            }
+        }
+        __device__ Tile tile(uint32_t k, uint32_t slot, uint32_t ns) const {
+            const uint32_t b0 = x0 + (slot + k * ns) * uint32_t(W);
+            return {b0, b0 + uint32_t(W) < x1 ? b0 + uint32_t(W) : x1};
+        }
+    };
+
+    // ---------------- loader ----------------
+    struct Loader {
+        uint32_t off[BPL];  // layer(c, g) * sc + 16 * piece, per block
+        uint32_t pc16;      // 16 * piece
+    };
+    __device__ static void loader_init(Loader &L, uint32_t sc, int li, int lane) {
+        const uint32_t k = uint32_t(lane);
+        L.pc16 = (k & 3u) * 16u;
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            const uint32_t cc = uint32_t(li * BPL + j) * 4u + (k >> 4);
+            const uint32_t g = ((k >> 2) & 3u) ^ (k >> 4);
+            L.off[j] = (layer0(cc) + g * wt(G)) * sc + L.pc16;
+        }
+    }
+    __device__ static void issue(const DecArgs &a, const Loader &L, uint32_t lds_buf, const uint8_t *node, Tile t,
+                                 int li) {
+        if (t.vend >= t.b0 + uint32_t(W)) {
+            const uint8_t *base = uniform_ptr(node + t.b0);
+#pragma unroll
+            for (int j = 0; j < BPL; j++) dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.off[j]);
+        } else {
+            // partial tile: a piece straddling vend is read from vend - 16 (the compute lane
+            // of that part reads the slot's upper half), a piece wholly past vend from b0
+            const uint8_t *base = uniform_ptr(node);
+            uint32_t pos = t.b0 + L.pc16;
+            if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
+#pragma unroll
+            for (int j = 0; j < BPL; j++)
+                dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.off[j] - L.pc16 + pos);
+        }
+    }
+};
+
+// PROBE (bench_tools / CLAY_DECODE_PROBE only; the product runs PROBE = 0): bit 1 = no phase-B
+// work (rounds keep their barriers), 2 = no phase-A math, 4 = loaders issue no DMA.
+template <int KD, int G, int PROBE = 0>
+__global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(DecArgs a) {
+    using Kn = StreamDec<KD, G>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7u, wslot = blockIdx.x >> 3, ns = a.nslots;
+    const uint32_t sc = uint32_t(a.sc);
+    const typename Kn::Map tm(sc, a.region, ns, xcd, wslot);
+    const uint32_t ntile = tm.n;
+    if (ntile == 0) return;  // uniform per workgroup
+    const uint32_t R = a.ring, NT = a.nt, nround = a.nround;
+    constexpr uint32_t BUF = uint32_t(Kn::BUF);
+
+    if (wave >= Kn::CWAVES) {
+        // ---------------- loader waves ----------------
+        // Tile-relative ring: load q of a tile goes to buffer q % R.  Within a tile a load is
+        // issued once the step that last used its buffer is done; the next tile's first R - 4
+        // loads are issued during phase B (buffers outside the S/C region), the rest after it.
+        __builtin_amdgcn_s_setprio(3);
+        const int li = wave - Kn::CWAVES;
+        typename Kn::Loader L;
+        Kn::loader_init(L, sc, li, lane);
+        const uint32_t lds0 = lds_addr_of(smem);
+        uint32_t issued = 0;  // loads issued in total (all tiles)
+        auto issue_upto = [&](uint32_t k, uint32_t lim) {  // tile k, tile-relative limit
+            if (k >= ntile) return;
+            if (lim > NT) lim = NT;
+            const typename Kn::Tile t = tm.tile(k, wslot, ns);
+            for (uint32_t q = issued - k * NT; q < lim; q++, issued++) {
+                const uint32_t nd = a.load_node[q];
+                if constexpr (!(PROBE & 4)) Kn::issue(a, L, lds0 + (q % R) * BUF, a.node[nd], t, li);
+            }
+        };
+        issue_upto(0, R);
+        for (uint32_t k = 0; k < ntile; k++) {
+            for (int y = 0; y < 4; y++) {
+                // loads of step (k, y) landed: everything issued after them may stay in flight
+                const uint32_t qend = k * NT + a.sec_off[y + 1];
+                wait_vm_rt(int((issued - qend) * uint32_t(Kn::BPL)));
+                lds_barrier();
+                issue_upto(k, a.sec_off[y] + R);  // steps before (k, y) are done
+            }
+            lds_barrier();  // B0: every step of tile k done -> S/C region written
+            {   // phase-B tables into buffer R - 5 (3 KiB: one 1 KiB block per loader wave 0..2)
+                if (li < 3) dma16(lds0 + (R - 5u) * BUF + uint32_t(li) * 1024u, uniform_ptr(reinterpret_cast<const uint8_t *>(a.tabs)),
+                                  uint32_t(li) * 1024u + uint32_t(lane) * 16u);
+                issue_upto(k + 1, R - 5);
+                // the tables landed (the prefetch issued after them may stay in flight)
+                wait_vm_rt(int((issued - (k + 1 < ntile ? (k + 1) * NT : issued)) * uint32_t(Kn::BPL)));
+            }
+            for (uint32_t rd = 0; rd < nround; rd++) lds_barrier();
+            lds_barrier();  // B_end: phase B done, the S/C region is free
+            issue_upto(k + 1, R);
+        }
+        wait_vm0();
+        return;
+    }
+
+    // ---------------- compute waves ----------------
+    const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
+    const uint32_t emG = a.emask[G];
+    const int xeG = emG ? __builtin_ctz(emG) : -1;
+    const int rG = emG ? a.rix[4 * G + xeG] : -1;
+    const uint32_t scbase = (R - 4u) * BUF, outbase = R * BUF;
+
+    for (uint32_t k = 0; k < ntile; k++) {
+        const typename Kn::Tile t = tm.tile(k, wslot, ns);
+        const bool straddle = t.vend < t.b0 + uint32_t(Kn::W) && ((t.vend - t.b0) & 15u) == 8u;
+        const uint32_t pcs = (t.vend - t.b0) >> 4;
+        const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
+
+        uint32_t S[32];
+#pragma unroll
+        for (int w = 0; w < 32; w++) S[w] = 0;
+
+        // ---------------- phase A: one step per section ----------------
+        sfor<4>([&](auto yc) BS_INL {
+            constexpr int Y = decltype(yc)::value;
+            lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
+            if constexpr ((PROBE & 2) != 0) return;
+            const uint32_t c = opq(c0), poff = opq(poff0);
+            const uint32_t aliveY = (a.alive >> (4 * Y)) & 15u;
+            const uint32_t rs = a.sec_off[Y];
+            auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
+                const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
+                return smem + (q % R) * BUF;
+            };
+            // Out(e, (c, g), p) of erased e: item layout [r][z][p] in the Out region
+            auto put_out = [&](int r, const uint32_t (&v)[8]) BS_INL {
+                uint8_t *ob = smem + outbase + uint32_t(r) * BUF + 8u * p;
+                const uint32_t z0 = Kn::layer0(c);
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    *reinterpret_cast<uint2 *>(ob + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) = make_uint2(v[2 * g], v[2 * g + 1]);
+            };
+            if constexpr (Y != G) {
+                constexpr int sh = Kn::csh(Y);
+                const uint32_t cy = (c >> sh) & 3u;
+                const bool comp_alive = (aliveY >> cy) & 1u;
+                const uint8_t *cbuf = comp_alive ? buf_of(cy) : smem;
+                sfor<4>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    constexpr int I = 4 * Y + X;
+                    const bool alive_i = (aliveY >> X) & 1u;
+                    const bool used_i = (a.used >> I) & 1u;
+                    const bool erased_i = (a.emask[Y] >> X) & 1u;
+                    if (!(used_i || erased_i)) return;
+                    uint32_t o[8], cv[8], u[8];
+                    if (alive_i) {
+                        Kn::read4(buf_of(X), c, poff, o);
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < 8; w++) o[w] = 0;
+                    }
+                    const uint32_t cc = (c & ~(3u << sh)) | (uint32_t(X) << sh);
+                    Kn::read4(cbuf, cc, poff, cv);
+                    const uint32_t keep = (comp_alive && cy != uint32_t(X)) ? 0xffffffffu : 0u;
+                    const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                    if (erased_i) {
+                        uint32_t v[8];
+#pragma unroll
+                        for (int w = 0; w < 8; w++) v[w] = xor_xtime4_masked(0u, cv[w], ks, kr);
+                        put_out(a.rix[I], v);
+                    }
+                    if (used_i) {
+#pragma unroll
+                        for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+                        transpose8(u);
+                        Kn::template fold<I, false>(u, S);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+            } else {
+                // section G: all four nodes' slots are in the lane; U(a, g) = C(a, g) + gamma C(g, a)
+                uint32_t o[4][8];
+                sfor<4>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    if ((aliveY >> X) & 1u) {
+                        Kn::read4(buf_of(X), c, poff, o[X]);
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < 8; w++) o[X][w] = 0;
+                    }
+                });
+                if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
+                    uint32_t v[8];
+                    sfor<4>([&](auto gc) BS_INL {
+                        constexpr int g = decltype(gc)::value;
+                        v[2 * g] = v[2 * g + 1] = 0;
+                        sfor<4>([&](auto ac) BS_INL {
+                            constexpr int A = decltype(ac)::value;
+                            if (A != g && xeG == A) {
+                                v[2 * g] = gf_xt(o[g][2 * A]);
+                                v[2 * g + 1] = gf_xt(o[g][2 * A + 1]);
+                            }
+                        });
+                    });
+                    put_out(rG, v);
+                }
+                sfor<4>([&](auto ac) BS_INL {
+                    constexpr int A = decltype(ac)::value;
+                    constexpr int I = 4 * G + A;
+                    if (!((a.used >> I) & 1u)) return;
+                    uint32_t u[8];
+                    sfor<4>([&](auto gc) BS_INL {
+                        constexpr int g = decltype(gc)::value;
+                        const uint32_t keep = (A != g && ((aliveY >> g) & 1u)) ? 0xffffffffu : 0u;
+                        const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                        u[2 * g] = xor_xtime4_masked(o[A][2 * g], o[g][2 * A], ks, kr);
+                        u[2 * g + 1] = xor_xtime4_masked(o[A][2 * g + 1], o[g][2 * A + 1], ks, kr);
+                    });
+                    transpose8(u);
+                    Kn::template fold<I, false>(u, S);
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+            }
+        });
+
+        // ---------------- S_known -> LDS (S/C region, [j][z][p]) ----------------
+        lds_barrier();  // B0: every wave is done with the ring buffers of tile k
+        {
+            const uint32_t c = opq(c0);
+            const uint32_t z0 = Kn::layer0(c);
+            sfor<4>([&](auto jc) BS_INL {
+                constexpr int j = decltype(jc)::value;
+                uint32_t v[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++) v[w] = S[j * 8 + w];
+                transpose8(v);
+                uint8_t *sb = smem + scbase + uint32_t(j) * BUF + 8u * p;
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    *reinterpret_cast<uint2 *>(sb + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) = make_uint2(v[2 * g], v[2 * g + 1]);
+            });
+        }
+
+        // ---------------- phase B: rounds in iscore order ----------------
+        // tables (v_perm, 8-dword stride) and the layer order in LDS buffer R - 5 (the loaders
+        // copied them after B0; visible after the first round's barrier)
+        const uint8_t *tl = smem + (R - 5u) * BUF;
+        auto tab = [&](int t) BS_INL {
+            const uint4 v = *reinterpret_cast<const uint4 *>(tl + t * 32);
+            GfTab r;
+            r.w0 = v.x;
+            r.w1 = v.y;
+            r.w2 = v.z;
+            r.w3 = v.w;
+            r.w4 = *reinterpret_cast<const uint32_t *>(tl + t * 32 + 16);
+            return r;
+        };
+        for (uint32_t rd = 0; rd < nround; rd++) {
+            lds_barrier();  // S of this tile / C of the previous round visible
+            const uint32_t li = a.round_start[rd] + opq(c0);
+            if (li >= a.round_start[rd + 1] || (PROBE & 1)) continue;
+            const uint32_t z = tl[kDecOrder * 4 + li];
+            const uint32_t pp = opq(p);
+            const uint8_t *scb = smem + scbase + z * 64u + 8u * pp;
+            // U_r = sum_j Hinv[e_r][j] * S_j
+            uint32_t U[4][2];
+#pragma unroll
+            for (int r = 0; r < 4; r++) U[r][0] = U[r][1] = 0;
+            sfor<4>([&](auto jc) BS_INL {
+                constexpr int j = decltype(jc)::value;
+                const uint2 sv = *reinterpret_cast<const uint2 *>(scb + j * BUF);
+                const GfIdx i0 = gf_idx(sv.x), i1 = gf_idx(sv.y);
+                sfor<4>([&](auto rc) BS_INL {
+                    constexpr int r = decltype(rc)::value;
+                    if (uint32_t(r) >= a.ne) return;
+                    const GfTab tb = tab(r * 4 + j);
+                    U[r][0] ^= gf_mul_idx(i0, tb);
+                    U[r][1] ^= gf_mul_idx(i1, tb);
+                });
+            });
+            // dropped terms: used nodes whose companion is the red erased node of section y
+            sfor<4>([&](auto yc) BS_INL {
+                constexpr int Y = decltype(yc)::value;
+                constexpr uint32_t wy = Kn::wt(Y);
+                const uint32_t zy = (z / wy) & 3u;
+                if (!((a.emask[Y] >> zy) & 1u)) return;
+                int ry = a.rix[4 * Y];
+#pragma unroll
+                for (int x = 1; x < 4; x++) ry = zy == uint32_t(x) ? a.rix[4 * Y + x] : ry;
+                const uint8_t *cb = smem + scbase + uint32_t(ry) * BUF + 8u * pp;
+                const uint32_t zb = z - zy * wy;
+                sfor<4>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    if (!((a.used >> (4 * Y + X)) & 1u) || uint32_t(X) == zy) return;
+                    const uint2 cv = *reinterpret_cast<const uint2 *>(cb + (zb + uint32_t(X) * wy) * 64u);
+                    const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
+                    sfor<4>([&](auto rc) BS_INL {
+                        constexpr int r = decltype(rc)::value;
+                        if (uint32_t(r) >= a.ne) return;
+                        const GfTab tb = tab(16 + (Y * 4 + X) * 4 + r);
+                        U[r][0] ^= gf_mul_idx(i0, tb);
+                        U[r][1] ^= gf_mul_idx(i1, tb);
+                    });
+                });
+            });
+            // C = U + Out (Out is 0 where e is red); into the item's S slots and HBM
+            const bool pvalid = t.b0 + 8u * pp + 8u <= t.vend;
+            sfor<4>([&](auto rc) BS_INL {
+                constexpr int r = decltype(rc)::value;
+                if (uint32_t(r) >= a.ne) return;
+                const uint2 ov = *reinterpret_cast<const uint2 *>(smem + outbase + r * BUF + z * 64u + 8u * pp);
+                const uint32_t c0v = U[r][0] ^ ov.x, c1v = U[r][1] ^ ov.y;
+                *reinterpret_cast<uint2 *>(smem + scbase + r * BUF + z * 64u + 8u * pp) = make_uint2(c0v, c1v);
+                uint8_t *dst = a.out[r];
+                if (dst && pvalid)
+                    *reinterpret_cast<uint2 *>(dst + (uint64_t(z) * sc + t.b0 + 8u * pp)) = make_uint2(c0v, c1v);
+            });
+        }
+        lds_barrier();  // B_end
+    }
+}
+
+}  // namespace bs
+}  // namespace clay

@@ -256,11 +256,14 @@ int clay_set_encode_path(int mode);
  *                per-level executor
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
+ *   3 stream  -- decode of q = 4, t = 4 codes ((10,4,13), (9,4,12)) on the single-launch
+ *                streaming decode kernel when the erasures sit in distinct y-sections and
+ *                sc % 8 == 0, sc >= 512 (last path "stream"); everything else as auto
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
  * unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
- * "tile" (k_texec), "grouped" (k_gexec) or "none". */
+ * "tile" (k_texec), "grouped" (k_gexec), "stream" (k_stream_decode) or "none". */
 const char *clay_last_exec_path(void);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
