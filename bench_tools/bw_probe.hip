@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <vector>
 
+#include "../clay_amd/csrc/bitslice.hpp"  // dma16, lds_barrier, wait_vm_rt (LDS-DMA helpers)
+
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #define CK(x)                                                            \
     do {                                                                 \
@@ -88,6 +90,81 @@ __global__ __launch_bounds__(B) void k_write_gs(v4u *__restrict__ d, size_t n) {
     for (; i < n; i += stride) d[i] = v;
 }
 
+// encode-like traffic mix: 5 reads per 2 writes (the (10,4) encode reads 10 chunks and writes 4)
+template <int U, int B, int MODE>
+__global__ __launch_bounds__(B) void k_mix_gs(const v4u *__restrict__ s, v4u *__restrict__ d, size_t n) {
+    const size_t stride = size_t(gridDim.x) * B;
+    size_t i = size_t(blockIdx.x) * B + threadIdx.x;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        v4u v[U][5];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) v[u][k] = s[i + u * stride + k * n];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const v4u w0 = v[u][0] ^ v[u][1] ^ v[u][2], w1 = v[u][3] ^ v[u][4] ^ v[u][0];
+            if (MODE & 2) {
+                __builtin_nontemporal_store(w0, d + i + u * stride);
+                __builtin_nontemporal_store(w1, d + i + u * stride + n);
+            } else {
+                d[i + u * stride] = w0;
+                d[i + u * stride + n] = w1;
+            }
+        }
+    }
+}
+
+// LDS-DMA copy with role-split waves, one workgroup per CU (the encode's structure): 4 loader
+// waves stream 16 KiB slots into an R-slot LDS ring with global_load_lds_dwordx4 and counted
+// vmcnt waits; 8 writer waves read each landed slot (ds_read_b128) and store it.  Each XCD
+// owns a contiguous region; its 32 workgroups take adjacent 16 KiB slots round robin.
+template <int R, int MODE>
+__global__ __launch_bounds__(768) void k_copy_dma(const uint8_t *__restrict__ s, uint8_t *__restrict__ d, size_t nbytes) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    using namespace clay::bs;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, ns = gridDim.x >> 3;
+    const size_t region = nbytes / 8, x0 = xcd * region;
+    const uint32_t nslot_total = uint32_t(region / 16384);
+    const uint32_t nsteps = nslot_total > slot ? (nslot_total - slot + ns - 1) / ns : 0;
+    auto src_of = [&](uint32_t k) { return x0 + (size_t(slot) + size_t(k) * ns) * 16384; };
+    if (wave < 4) {
+        const uint32_t lds0 = lds_addr_of(smem);
+        uint32_t issued = 0;
+        auto issue = [&](uint32_t k) {
+            const uint8_t *base = s + src_of(k);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                dma16(lds0 + (k % R) * 16384u + uint32_t(wave * 4 + j) * 1024u, base,
+                      uint32_t(wave * 4 + j) * 1024u + uint32_t(lane) * 16u);
+            issued++;
+        };
+        while (issued < nsteps && issued < uint32_t(R - 1)) issue(issued);
+        for (uint32_t k = 0; k < nsteps; k++) {
+            wait_vm_rt(int((issued - (k + 1)) * 4));
+            lds_barrier();
+            if (issued < nsteps && issued < k + uint32_t(R)) issue(issued);  // into slot (k-1) % R
+        }
+        return;
+    }
+    const int w = wave - 4;
+    for (uint32_t k = 0; k < nsteps; k++) {
+        lds_barrier();
+        const uint8_t *sl = smem + (k % R) * 16384u;
+        uint8_t *dst = d + src_of(k);
+        const v4u a0 = *reinterpret_cast<const v4u *>(sl + w * 2048 + lane * 16);
+        const v4u a1 = *reinterpret_cast<const v4u *>(sl + w * 2048 + 1024 + lane * 16);
+        if (MODE & 2) {
+            __builtin_nontemporal_store(a0, reinterpret_cast<v4u *>(dst + w * 2048 + lane * 16));
+            __builtin_nontemporal_store(a1, reinterpret_cast<v4u *>(dst + w * 2048 + 1024 + lane * 16));
+        } else {
+            *reinterpret_cast<v4u *>(dst + w * 2048 + lane * 16) = a0;
+            *reinterpret_cast<v4u *>(dst + w * 2048 + 1024 + lane * 16) = a1;
+        }
+    }
+}
+
 template <class F>
 static float timeit(F &&launch, int reps = 14) {
     hipEvent_t e0, e1;
@@ -163,5 +240,29 @@ int main() {
     WRITE(8, 256, 0, 2048)
     WRITE(4, 256, 2, 4096)
     rep("hipMemsetAsync 2 GiB", 2.0 * G, timeit([&] { (void)hipMemsetAsync(b, 3, 2 * G, 0); }));
+    // role-split LDS-DMA copy (loader + writer waves per CU, the encode's structure)
+    int cus = 256;
+    {
+        hipDeviceProp_t pr;
+        if (hipGetDeviceProperties(&pr, 0) == hipSuccess) cus = pr.multiProcessorCount;
+    }
+#define COPYDMA(R, MODE)                                                                                         \
+    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_copy_dma<R, MODE>),                              \
+                           hipFuncAttributeMaxDynamicSharedMemorySize, R * 16384));                          \
+    snprintf(nm, sizeof nm, "copy lds-dma R%d mode%d grid%d", R, MODE, cus);                                  \
+    rep(nm, 2.0 * G, timeit([&] { k_copy_dma<R, MODE><<<cus, 768, R * 16384>>>(a, b, G); }));
+    COPYDMA(4, 0)
+    COPYDMA(8, 0)
+    COPYDMA(9, 0)
+    COPYDMA(8, 2)
+    // the encode's traffic mix: 5 reads : 2 writes
+    const size_t nm5 = G / 80;  // 5 * nm5 * 16 B = 1 GiB read, 2 * nm5 * 16 B written
+#define MIX(U, B, MODE, GRID)                                                                                    \
+    snprintf(nm, sizeof nm, "mix 5r:2w U%d B%d mode%d grid%d", U, B, MODE, GRID);                           \
+    rep(nm, 7.0 * nm5 * 16, timeit([&] { k_mix_gs<U, B, MODE><<<GRID, B>>>((const v4u *)a, (v4u *)b, nm5); }));
+    MIX(1, 256, 0, 8192)
+    MIX(2, 256, 0, 4096)
+    MIX(2, 256, 2, 4096)
+    MIX(4, 256, 0, 2048)
     return 0;
 }

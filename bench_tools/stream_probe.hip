@@ -70,6 +70,8 @@ int main(int argc, char **argv) {
             rep("L4 no math (memory only)", run<4, 1>(a, 15));
             rep("L4 reads", run<4, 5>(a, 15));
             rep("L4 stores only", run<4, 3>(a, 15));
+            rep("L4 memory only, rotated stores", run<4, 33>(a, 15));
+            rep("L4 stores only, rotated", run<4, 35>(a, 15));
         }
         return 0;
     }

@@ -711,6 +711,10 @@ static Error lease_acquire(DevState &ds, size_t bytes, hipStream_t st, Lease **o
     std::lock_guard<std::mutex> lk(ds.mu);
     const bool cap = capturing(st);
     Lease *best = nullptr;
+    if (!cap)  // idle buffers whose last use has completed are free for any stream (and for a
+               // later stream capture, which may not query events or allocate)
+        for (auto &l : ds.pool)
+            if (!l->busy && !l->pinned && l->used && event_done(l->ev)) l->used = false;
     for (auto &l : ds.pool) {
         if (l->busy || l->pinned || l->bytes < bytes || (best && l->bytes >= best->bytes)) continue;
         if (!l->used || l->last == st || (!cap && event_done(l->ev))) best = l.get();
@@ -1965,6 +1969,18 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
 }
 
+// repair_stream.hip: bit-sliced repair kernel (repair_kernel.hpp); 1 launched, 0 no
+// instantiation for (k, m), < 0 HIP error
+namespace bs {
+struct RepArgs {
+    const uint8_t *h[16];
+    uint8_t *out;
+    uint64_t sc;
+    uint32_t x0, full, ntiles, per_xcd;
+};
+}  // namespace bs
+int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream);
+
 static Error repair_device_impl(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs,
                                 const size_t *lens, size_t nh, size_t chunk, uint8_t *out, int dev, void *stream,
                                 bool full = false) {
@@ -1986,6 +2002,32 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
     if (tn > size_t(kMaxTn))
         return make_error(CLAY_ERR_DEVICE, tn, 0, 0, "device engine supports at most %d internal nodes", kMaxTn);
     CodeState &cs = *code_state(c);
+    // bit-sliced single-launch repair (repair_kernel.hpp): q = m codes with every other node a
+    // helper (no aloof nodes); "stream" exec mode
+    if (g_exec_mode.load(std::memory_order_relaxed) == kExecStream && c.q == c.m && tn <= 16 &&
+        nh + 1 == c.n) {
+        bs::RepArgs ra{};
+        const size_t lost_int = internal_of(c, lost);
+        bool ok = true;
+        for (size_t in = 0; in < tn; in++) {
+            if (in == lost_int || (in >= c.k && in < c.k + c.nu)) continue;
+            if (slot_of[in] < 0) ok = false;
+            else ra.h[in] = bufs[slot_of[in]];
+        }
+        if (ok) {
+            ra.out = out;
+            ra.sc = chunk / c.sub_chunk_no;
+            ra.x0 = uint32_t(lost_int % c.q);
+            ra.full = full ? 1u : 0u;
+            const int r = launch_bs_repair_kernel(int(c.k), int(c.m), int(lost_int / c.q), ra, static_cast<hipStream_t>(stream));
+            if (r < 0) return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: %s", hipGetErrorString(hipError_t(-r)));
+            if (r > 0) {
+                t_last_launches++;
+                t_last_exec = "bs-repair";
+                return Error{};
+            }
+        }
+    }
     std::vector<uint8_t> key(hin);
     key.push_back(uint8_t(lost & 0xFF));
     key.push_back(uint8_t(lost >> 8));
@@ -2333,7 +2375,11 @@ int clay_reserve_workspace(const clay_code_t *code, size_t chunk, int device, cl
     Lease *l = nullptr;
     e = lease_acquire(*ds, code->q * code->t * chunk, nullptr, &l);
     if (e) return report(e, err);
-    lease_release(*ds, l, nullptr);
+    {   // nothing was enqueued on it: hand it back unused, so that any stream -- also one that is
+        // capturing a graph (no event query or allocation while capturing) -- may take it
+        std::lock_guard<std::mutex> lk(ds->mu);
+        l->busy = false;
+    }
     CodeState &cs = *code_state(*code);
     const Plan *pl = nullptr;
     CodeState::DevGrouped gp{};

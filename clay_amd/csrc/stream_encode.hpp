@@ -364,7 +364,9 @@ struct StreamEnc {
 // XCD; grid = 8 * nslots; LDS = KD x 16 KiB (one workgroup per CU).
 // PROBE is for bench_tools/stream_probe.hip only (the library instantiates PROBE = 0):
 // bit 1 = compute waves skip the math, 2 = loaders skip the DMA, 4 = no parity stores,
-// 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1.
+// 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1, 32 = the group whose
+// outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
+// across workgroups; only meaningful with bit 1).
 template <int KD, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
     using Kn = StreamEnc<KD, LOADERS>;
@@ -478,12 +480,13 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         if (y == 2 && !(PROBE & 4)) {
             const StreamTile t = tm.tile(k, slot, ns);
             const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
-            if (g == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged);
-            else if (g == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged);
-            else if (g == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged);
+            const int ge = (PROBE & 32) ? ((g + int(slot)) & 3) : g;
+            if (ge == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged);
+            else if (ge == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged);
+            else if (ge == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged);
             else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged);
             st2 = st1;
-            st1 = ragged ? 0 : Kn::nstores(g);  // a ragged tile's plain stores are not counted:
+            st1 = ragged ? 0 : Kn::nstores(ge);  // a ragged tile's plain stores are not counted:
                                                  // the waits then cover more than needed
         } else {
             st2 = st1;

@@ -252,7 +252,9 @@ def test_non_affine_table_across_streams_and_capture(oracle_mod, torch_cuda):
     sb.synchronize()
     sa.synchronize()
     check(pars[0], "A then B")
-    # a table first seen inside a capture, then the same pointer set eagerly on D
+    # a table first seen inside a capture, then the same pointer set eagerly on D (the capture
+    # takes an idle reserved workspace: nothing may be allocated while capturing)
+    c.reserve_workspace(n * chunk)  # the batch's U workspace: tn x chunk per stripe
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=sc_):
         c.encode_device_batch(dl, pl(pars[1]), n, chunk, 0, torch.cuda.current_stream().cuda_stream)
