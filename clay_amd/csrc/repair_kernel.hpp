@@ -176,40 +176,37 @@ struct BsRepair {
                         cp = a.h[Y * Q + X];
                     }
                 });
-                // all loads of the section first (straight-line: the loads overlap), then the math
-                uint32_t o[Q][8], cv[Q][8];
-                uint32_t keepm[Q];
                 sfor<Q>([&](auto xc) BS_INL {
                     constexpr int X = decltype(xc)::value;
                     constexpr int I = Y * Q + X;
+                    uint32_t o[8], cv[8];
                     const bool keep = creal && zy != uint32_t(X);
-                    keepm[X] = keep ? 0xffffffffu : 0u;
                     const uint8_t *op = real(I) ? row(I, j) : nullptr;
                     const uint32_t jc = j + (uint32_t(X) - zy) * jw(Y);
                     const uint64_t l = a.full ? uint64_t(layer_of(jc, x0)) : uint64_t(jc);
-                    // a masked companion is read from a valid row (its own) and discarded
-                    const uint8_t *cq = keep ? cp + l * sc + pos : (real(I) ? op : a.out + pos);
                     if constexpr (FULL) {
-                        if constexpr (real(I)) ld32v(o[X], op);
-                        ld32v(cv[X], cq);
+                        // a masked companion is read from a valid row (its own) and discarded:
+                        // no branch around the load, so loads of consecutive nodes overlap
+                        const uint8_t *cq = keep ? cp + l * sc + pos : (real(I) ? op : a.out + pos);
+                        if constexpr (real(I)) ld32v(o, op);
+                        ld32v(cv, cq);
                     } else {
-                        if constexpr (real(I)) ld32<false, true>(o[X], op, nv);
-                        if (keep) ld32<false, true>(cv[X], cq, nv);
-                        else
+                        if constexpr (real(I)) ld32<false, true>(o, op, nv);
+                        if (keep) {
+                            ld32<false, true>(cv, cp + l * sc + pos, nv);
+                        } else {
 #pragma unroll
-                            for (int w = 0; w < 8; w++) cv[X][w] = 0;
+                            for (int w = 0; w < 8; w++) cv[w] = 0;
+                        }
                     }
                     if constexpr (!real(I)) {
 #pragma unroll
-                        for (int w = 0; w < 8; w++) o[X][w] = 0;
+                        for (int w = 0; w < 8; w++) o[w] = 0;
                     }
-                });
-                sfor<Q>([&](auto xc) BS_INL {
-                    constexpr int X = decltype(xc)::value;
-                    constexpr int I = Y * Q + X;
+                    const uint32_t km = keep ? 0xffffffffu : 0u;
                     uint32_t u[8];
 #pragma unroll
-                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4(o[X][w], cv[X][w] & keepm[X]);
+                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4(o[w], cv[w] & km);
                     transpose8(u);
                     fold<I>(u, acc);
                 });

@@ -256,6 +256,8 @@ int clay_set_encode_path(int mode);
  *                per-level executor
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
+ *   (auto and stream: repair of (9,3,11), (10,4,13), (4,2,5) from all n - 1 other nodes runs
+ *    the bit-sliced repair kernel k_bs_repair, last path "bs-repair")
  *   3 stream  -- decode of q = 4, t = 4 codes ((10,4,13), (9,4,12)) on the single-launch
  *                streaming decode kernel when the erasures sit in distinct y-sections and
  *                sc % 8 == 0, sc >= 512 (last path "stream"); everything else as auto
@@ -263,7 +265,8 @@ int clay_set_encode_path(int mode);
  * unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
- * "tile" (k_texec), "grouped" (k_gexec), "stream" (k_stream_decode) or "none". */
+ * "tile" (k_texec), "grouped" (k_gexec), "stream" (k_stream_decode), "bs-repair"
+ * (k_bs_repair) or "none". */
 const char *clay_last_exec_path(void);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */

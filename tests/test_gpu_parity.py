@@ -195,9 +195,9 @@ def test_repair_every_node_matches_oracle(oracle_mod, cfg, exec_mode):
 @pytest.mark.parametrize("cfg,lost,mode,launches", [((9, 3, 11), 0, "tile", 1), ((4, 2, 5), 3, "auto", 1),
                                                      ((10, 4, 13), 0, "tile", 1), ((9, 3, 11), 0, "auto", 1)])
 def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
-    """'tile' runs repair plans whose U slots fit in LDS as ONE tile-fused launch, 'auto'
-    only small multi-level plans ((9,3,11) repair is a single folded level: one k_gexec
-    launch); the bytes equal the grouped executor's and the oracle's."""
+    """'tile' runs repair plans whose U slots fit in LDS as ONE tile-fused launch; 'auto' runs
+    the bit-sliced repair kernel (one launch) for the q = m codes it is instantiated for; the
+    bytes equal the grouped executor's and the oracle's."""
     k, m, d = cfg
     c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
     sc = 16 * 100 + 6
@@ -210,8 +210,7 @@ def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
     try:
         got = c.repair(lost, pr, chunk)
         assert clay_amd.last_launch_count() == launches
-        # repair plans are one folded level: auto keeps them on the grouped executor
-        assert clay_amd.last_exec_path() == ("tile" if mode == "tile" else "grouped")
+        assert clay_amd.last_exec_path() == ("tile" if mode == "tile" else "bs-repair")
         clay_amd.set_exec_mode("grouped")
         assert c.repair(lost, pr, chunk) == got
     finally:
