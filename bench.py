@@ -40,8 +40,10 @@ sys.path.insert(0, ROOT)
 K, M, D = 10, 4, 13
 STRIPE_BYTES = 1 << 30  # reference ClayCode::encode input
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-# best copy kernel measured on this pool (bench_tools/bw_probe.hip, profiles/r02_probes/bw_probe_r02a.txt)
-COPY_CEILING_GBS = 5418.0
+# best copy kernel measured on this pool: LDS-DMA loader waves + writer waves per CU, nt stores
+# (bench_tools/bw_probe.hip, profiles/r03/bw_probe_r03.txt; the encode's own 5:2 read/write mix
+# streams at 5,090 GB/s with plain loads/stores in the same sweep)
+COPY_CEILING_GBS = 5546.0
 VERIFY_W = 4096         # positions per verified column slice (every rank, both ends)
 
 

@@ -18,7 +18,7 @@ struct DecArgs {
     uint32_t ne;              // erased count (1..4)
     int32_t rix[16];          // erased index r of internal node i, else -1
     uint32_t emask[4];        // per section y: bit x set if node (y, x) is erased
-    uint32_t ring;            // staging ring buffers R = 10 - ne
+    uint32_t ring;            // staging ring buffers R = 10
     uint32_t nt;              // loads per tile (alive nodes)
     uint32_t sec_off[5];      // first load of section y's step within a tile
     uint32_t load_node[16];   // internal node of each load of a tile

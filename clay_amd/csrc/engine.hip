@@ -1839,7 +1839,7 @@ static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uin
         }
     }
     a.used = used;
-    const uint32_t R = 10 - a.ne;
+    const uint32_t R = 10;
     uint32_t n[4] = {0, 0, 0, 0}, nt = 0;
     for (int y = 0; y < 4; y++) {
         a.sec_off[y] = nt;
@@ -1861,7 +1861,7 @@ static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uin
     if (R < 5) return Error{};  // S/C region (4 buffers) + the phase-B table buffer
     a.ring = R;
     // phase-B layer order: by iscore level (red erased sections), then by the set of red
-    // sections (uniform corrections per wave), rounds of <= 64 layers of one level
+    // sections (uniform corrections per wave), rounds of <= 128 layers of one level
     std::vector<std::pair<uint32_t, int>> lay;
     for (int z = 0; z < 256; z++) {
         uint32_t red = 0;
@@ -1875,7 +1875,7 @@ static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uin
     for (size_t i = 0; i < lay.size(); i++) {
         ord[i] = uint8_t(lay[i].second);
         const bool new_level = i == 0 || (lay[i].first >> 8) != (lay[i - 1].first >> 8);
-        if (new_level || i - a.round_start[nr - 1] >= 64) {
+        if (new_level || i - a.round_start[nr - 1] >= 128) {  // two layers per lane octet
             if (nr + 1 >= sizeof(a.round_start) / sizeof(a.round_start[0])) return Error{};
             a.round_start[nr++] = uint32_t(i);
         }

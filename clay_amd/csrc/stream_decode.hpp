@@ -14,9 +14,10 @@
 // z' is solved, so:
 //   phase A (streaming): S_known(z) = sum_i H_i U'(i, z) with those terms dropped, and
 //            Out(e, z) = gamma * C(companion of e at z) for erased e (compute_c_from_u_and_cstar)
-//   phase B (rounds in iscore order): U_e(z) = row e of H_K^-1 S_known(z)
-//            + sum over the dropped terms A_(y,x)[e] C(e_y, z[y:=x])  (A = H_K^-1 gamma H_(y,x)),
-//            C(e, z) = U_e(z) + Out(e, z)  (Out = 0 where e is red).
+//   phase B (rounds in iscore order): C(e, z) = row e of H_K^-1 S(z)
+//            + sum over the dropped terms A_(y,x)[e] C(e_y, z[y:=x])  (A = H_K^-1 gamma H_(y,x)).
+// Out needs no storage: S += H_e Out(e, z) in phase A (H_K H_K^-1 = I, so row e of H_K^-1 S
+// becomes U_e + Out_e = C_e directly; Out = 0 where e is red).
 //
 // Phase A tile and lane map.  A workgroup owns W = 64 byte positions of every (node, layer) row.
 // Section G (template, 3) is the lane's "slot" digit: lane (column c = the other three digits,
@@ -33,9 +34,9 @@
 // item's own S slots.  The iscore dependency therefore costs a few short rounds instead of
 // divergent passes over every lane.
 //
-// LDS (10 x 16 KiB): ring of R = 10 - ne node buffers; Out(e, ., .) in the top ne buffers; during
-// phase B the S/C region (4 x 16 KiB, [j][z][p] x 8 B) reuses ring buffers R-4 .. R-1 while the
-// loaders prefetch the next tile's first nodes into buffers 0 .. R-5.
+// LDS (10 x 16 KiB): a ring of R = 10 node buffers; during phase B the S/C region (4 x 16 KiB,
+// [j][z][p] x 8 B) reuses buffers R-4 .. R-1 and the tables buffer R-5, while the loaders
+// prefetch the next tile's first five nodes into buffers 0 .. R-6.
 #pragma once
 
 #include "decode_args.hpp"
@@ -243,8 +244,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
     const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
     const uint32_t emG = a.emask[G];
     const int xeG = emG ? __builtin_ctz(emG) : -1;
-    const int rG = emG ? a.rix[4 * G + xeG] : -1;
-    const uint32_t scbase = (R - 4u) * BUF, outbase = R * BUF;
+    const uint32_t scbase = (R - 4u) * BUF;
 
     for (uint32_t k = 0; k < ntile; k++) {
         const typename Kn::Tile t = tm.tile(k, wslot, ns);
@@ -267,14 +267,6 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
             auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
                 const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
                 return smem + (q % R) * BUF;
-            };
-            // Out(e, (c, g), p) of erased e: item layout [r][z][p] in the Out region
-            auto put_out = [&](int r, const uint32_t (&v)[8]) BS_INL {
-                uint8_t *ob = smem + outbase + uint32_t(r) * BUF + 8u * p;
-                const uint32_t z0 = Kn::layer0(c);
-#pragma unroll
-                for (int g = 0; g < 4; g++)
-                    *reinterpret_cast<uint2 *>(ob + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) = make_uint2(v[2 * g], v[2 * g + 1]);
             };
             if constexpr (Y != G) {
                 constexpr int sh = Kn::csh(Y);
@@ -299,11 +291,12 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
                     Kn::read4(cbuf, cc, poff, cv);
                     const uint32_t keep = (comp_alive && cy != uint32_t(X)) ? 0xffffffffu : 0u;
                     const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
-                    if (erased_i) {
+                    if (erased_i) {  // S += H_e Out(e, z): Out = gamma * companion (0 where red)
                         uint32_t v[8];
 #pragma unroll
                         for (int w = 0; w < 8; w++) v[w] = xor_xtime4_masked(0u, cv[w], ks, kr);
-                        put_out(a.rix[I], v);
+                        transpose8(v);
+                        Kn::template fold<I, false>(v, S);
                     }
                     if (used_i) {
 #pragma unroll
@@ -338,7 +331,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
                             }
                         });
                     });
-                    put_out(rG, v);
+                    transpose8(v);
+                    sfor<4>([&](auto ac) BS_INL {  // S += H_eG Out(e_G, .)
+                        constexpr int A = decltype(ac)::value;
+                        if (A == xeG) Kn::template fold<4 * G + A, false>(v, S);
+                    });
                 }
                 sfor<4>([&](auto ac) BS_INL {
                     constexpr int A = decltype(ac)::value;
@@ -393,63 +390,79 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
         };
         for (uint32_t rd = 0; rd < nround; rd++) {
             lds_barrier();  // S of this tile / C of the previous round visible
-            const uint32_t li = a.round_start[rd] + opq(c0);
-            if (li >= a.round_start[rd + 1] || (PROBE & 1)) continue;
-            const uint32_t z = tl[kDecOrder * 4 + li];
-            const uint32_t pp = opq(p);
-            const uint8_t *scb = smem + scbase + z * 64u + 8u * pp;
-            // U_r = sum_j Hinv[e_r][j] * S_j
-            uint32_t U[4][2];
+            if (PROBE & 1) continue;
+            // up to two items per lane: layers round_start + lane/8 and + 64 (independent)
+            sfor<2>([&](auto hc) BS_INL {
+                constexpr int hh = decltype(hc)::value;
+                const uint32_t li = a.round_start[rd] + opq(c0) + 64u * hh;
+                if (li >= a.round_start[rd + 1]) return;
+                const uint32_t z = tl[kDecOrder * 4 + li];
+                const uint32_t pp = opq(p);
+                const uint8_t *scb = smem + scbase + z * 64u + 8u * pp;
+                // C_r = sum_j Hinv[e_r][j] * S_j (+ the dropped terms below)
+                uint32_t U[4][2];
 #pragma unroll
-            for (int r = 0; r < 4; r++) U[r][0] = U[r][1] = 0;
-            sfor<4>([&](auto jc) BS_INL {
-                constexpr int j = decltype(jc)::value;
-                const uint2 sv = *reinterpret_cast<const uint2 *>(scb + j * BUF);
-                const GfIdx i0 = gf_idx(sv.x), i1 = gf_idx(sv.y);
+                for (int r = 0; r < 4; r++) U[r][0] = U[r][1] = 0;
+                // straight-line (no per-row branches: rows r >= ne use zero tables), so the
+                // compiler can keep many LDS table reads in flight
+                uint2 sv[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) sv[j] = *reinterpret_cast<const uint2 *>(scb + j * BUF);
+                GfTab tb[2][4];  // tables of check j + 1 are read while check j multiplies
+#pragma unroll
+                for (int r = 0; r < 4; r++) tb[0][r] = tab(r * 4);
+                sfor<4>([&](auto jc) BS_INL {
+                    constexpr int j = decltype(jc)::value;
+                    if constexpr (j + 1 < 4) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) tb[(j + 1) & 1][r] = tab(r * 4 + j + 1);
+                    }
+                    const GfIdx i0 = gf_idx(sv[j].x), i1 = gf_idx(sv[j].y);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        U[r][0] ^= gf_mul_idx(i0, tb[j & 1][r]);
+                        U[r][1] ^= gf_mul_idx(i1, tb[j & 1][r]);
+                    }
+                });
+                // dropped terms: used nodes whose companion is the red erased node of section y
+                sfor<4>([&](auto yc) BS_INL {
+                    constexpr int Y = decltype(yc)::value;
+                    constexpr uint32_t wy = Kn::wt(Y);
+                    const uint32_t zy = (z / wy) & 3u;
+                    if (!((a.emask[Y] >> zy) & 1u)) return;
+                    int ry = a.rix[4 * Y];
+#pragma unroll
+                    for (int x = 1; x < 4; x++) ry = zy == uint32_t(x) ? a.rix[4 * Y + x] : ry;
+                    const uint8_t *cb = smem + scbase + uint32_t(ry) * BUF + 8u * pp;
+                    const uint32_t zb = z - zy * wy;
+                    sfor<4>([&](auto xc) BS_INL {
+                        constexpr int X = decltype(xc)::value;
+                        // masked instead of branched (straight-line code, see above)
+                        const uint32_t m = (((a.used >> (4 * Y + X)) & 1u) && uint32_t(X) != zy) ? 0xffffffffu : 0u;
+                        uint2 cv = *reinterpret_cast<const uint2 *>(cb + (zb + uint32_t(X) * wy) * 64u);
+                        GfTab tc[4];
+#pragma unroll
+                        for (int r = 0; r < 4; r++) tc[r] = tab(16 + (Y * 4 + X) * 4 + r);
+                        cv.x &= m;
+                        cv.y &= m;
+                        const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            U[r][0] ^= gf_mul_idx(i0, tc[r]);
+                            U[r][1] ^= gf_mul_idx(i1, tc[r]);
+                        }
+                    });
+                });
+                // C into the item's S slots (for later rounds) and HBM
+                const bool pvalid = t.b0 + 8u * pp + 8u <= t.vend;
                 sfor<4>([&](auto rc) BS_INL {
                     constexpr int r = decltype(rc)::value;
                     if (uint32_t(r) >= a.ne) return;
-                    const GfTab tb = tab(r * 4 + j);
-                    U[r][0] ^= gf_mul_idx(i0, tb);
-                    U[r][1] ^= gf_mul_idx(i1, tb);
+                    *reinterpret_cast<uint2 *>(smem + scbase + r * BUF + z * 64u + 8u * pp) = make_uint2(U[r][0], U[r][1]);
+                    uint8_t *dst = a.out[r];
+                    if (dst && pvalid)
+                        *reinterpret_cast<uint2 *>(dst + (uint64_t(z) * sc + t.b0 + 8u * pp)) = make_uint2(U[r][0], U[r][1]);
                 });
-            });
-            // dropped terms: used nodes whose companion is the red erased node of section y
-            sfor<4>([&](auto yc) BS_INL {
-                constexpr int Y = decltype(yc)::value;
-                constexpr uint32_t wy = Kn::wt(Y);
-                const uint32_t zy = (z / wy) & 3u;
-                if (!((a.emask[Y] >> zy) & 1u)) return;
-                int ry = a.rix[4 * Y];
-#pragma unroll
-                for (int x = 1; x < 4; x++) ry = zy == uint32_t(x) ? a.rix[4 * Y + x] : ry;
-                const uint8_t *cb = smem + scbase + uint32_t(ry) * BUF + 8u * pp;
-                const uint32_t zb = z - zy * wy;
-                sfor<4>([&](auto xc) BS_INL {
-                    constexpr int X = decltype(xc)::value;
-                    if (!((a.used >> (4 * Y + X)) & 1u) || uint32_t(X) == zy) return;
-                    const uint2 cv = *reinterpret_cast<const uint2 *>(cb + (zb + uint32_t(X) * wy) * 64u);
-                    const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
-                    sfor<4>([&](auto rc) BS_INL {
-                        constexpr int r = decltype(rc)::value;
-                        if (uint32_t(r) >= a.ne) return;
-                        const GfTab tb = tab(16 + (Y * 4 + X) * 4 + r);
-                        U[r][0] ^= gf_mul_idx(i0, tb);
-                        U[r][1] ^= gf_mul_idx(i1, tb);
-                    });
-                });
-            });
-            // C = U + Out (Out is 0 where e is red); into the item's S slots and HBM
-            const bool pvalid = t.b0 + 8u * pp + 8u <= t.vend;
-            sfor<4>([&](auto rc) BS_INL {
-                constexpr int r = decltype(rc)::value;
-                if (uint32_t(r) >= a.ne) return;
-                const uint2 ov = *reinterpret_cast<const uint2 *>(smem + outbase + r * BUF + z * 64u + 8u * pp);
-                const uint32_t c0v = U[r][0] ^ ov.x, c1v = U[r][1] ^ ov.y;
-                *reinterpret_cast<uint2 *>(smem + scbase + r * BUF + z * 64u + 8u * pp) = make_uint2(c0v, c1v);
-                uint8_t *dst = a.out[r];
-                if (dst && pvalid)
-                    *reinterpret_cast<uint2 *>(dst + (uint64_t(z) * sc + t.b0 + 8u * pp)) = make_uint2(c0v, c1v);
             });
         }
         lds_barrier();  // B_end
