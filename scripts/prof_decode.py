@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """One decode (10,4,13) 1 GiB with 4 erasures {0,4,8,12} (and optionally repair (9,3,11)),
-repeated --iters times, for rocprofv3 --pmc passes (HBM bytes of the grouped executor)."""
+repeated --iters times, for rocprofv3 --pmc passes (HBM bytes per launch; CLAY_EXEC picks the
+executor: auto = grouped decode / bs-repair, stream = streaming decode)."""
 import argparse
 import os
 import sys
@@ -8,7 +9,10 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import clay_amd  # noqa: E402
 from clay_amd import ClayCode  # noqa: E402
+
+clay_amd.set_exec_mode(os.environ.get("CLAY_EXEC", "auto"))  # auto | grouped | tile | stream
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=4)
