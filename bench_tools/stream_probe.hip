@@ -63,6 +63,24 @@ int main(int argc, char **argv) {
     };
     for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
     (void)hipDeviceSynchronize();
+    if (argc > 2 && argv[2][0] == 'c') {  // cache-policy A/B (PROBE bits 64..512)
+        printf("sc %u cache policies\n", sc);
+        for (int rr = 0; rr < 2; rr++) {
+            rep("L4 full", run<4, 0>(a, 15));
+            rep("L4 full, nt loads", run<4, 64>(a, 15));
+            rep("L4 full, nt stores", run<4, 256>(a, 15));
+            rep("L4 full, nt loads + stores", run<4, 320>(a, 15));
+            rep("L4 full, sc1 loads", run<4, 128>(a, 15));
+            rep("L4 full, sc1 stores", run<4, 512>(a, 15));
+            rep("L4 memory only", run<4, 1>(a, 15));
+            rep("L4 memory only, nt loads", run<4, 65>(a, 15));
+            rep("L4 memory only, nt stores", run<4, 257>(a, 15));
+            rep("L4 memory only, nt both", run<4, 321>(a, 15));
+            rep("L4 reads, nt", run<4, 69>(a, 15));
+            rep("L4 stores only, nt", run<4, 259>(a, 15));
+        }
+        return 0;
+    }
     if (quick) {
         printf("sc %u\n", sc);
         for (int rr = 0; rr < 2; rr++) {

@@ -458,6 +458,21 @@ __device__ __forceinline__ void dma16(uint32_t lds_addr, const uint8_t *sbase, u
                  : "s"(lds_addr), "v"(voff), "s"(sbase)
                  : "memory");
 }
+// Cache-policy variants (bench_tools/stream_probe A/B): CP 1 = nt (streaming), 2 = sc1.
+template <int CP>
+__device__ __forceinline__ void dma16p(uint32_t lds_addr, const uint8_t *sbase, uint32_t voff) {
+    if constexpr (CP == 0) {
+        dma16(lds_addr, sbase, voff);
+    } else {
+        unsigned keep;
+        if constexpr (CP == 1)
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3 nt\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(sbase) : "memory");
+        else
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3 sc1\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(sbase) : "memory");
+    }
+}
 // 16-byte store, exactly one VMEM instruction.  s_nop 1: hipcc does not pad an asm
 // store's data hazard (the next instruction may overwrite the data VGPRs before the
 // store has read them).
@@ -470,6 +485,17 @@ __device__ __forceinline__ void st16s(const uint8_t *sbase, uint32_t voff, uint3
                                       uint32_t d) {
     const u32x4 v = {a, b, c, d};
     asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
+}
+template <int CP>
+__device__ __forceinline__ void st16sp(const uint8_t *sbase, uint32_t voff, uint32_t a, uint32_t b, uint32_t c,
+                                       uint32_t d) {
+    const u32x4 v = {a, b, c, d};
+    if constexpr (CP == 0)
+        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
+    else if constexpr (CP == 1)
+        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
+    else
+        asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(sbase) : "memory");
 }
 __device__ __forceinline__ uint32_t lds_addr_of(const void *p) {
     return uint32_t(size_t((__attribute__((address_space(3))) const uint8_t *)(p)));

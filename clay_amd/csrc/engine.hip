@@ -1977,9 +1977,11 @@ struct RepArgs {
     uint8_t *out;
     uint64_t sc;
     uint32_t x0, full, ntiles, per_xcd;
+    uint64_t b_start;
 };
 }  // namespace bs
-int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream);
+int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream, int dev, int cus,
+                            int stream_mode, int *launches);
 
 static Error repair_device_impl(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs,
                                 const size_t *lens, size_t nh, size_t chunk, uint8_t *out, int dev, void *stream,
@@ -2020,11 +2022,15 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
             ra.sc = chunk / c.sub_chunk_no;
             ra.x0 = uint32_t(lost_int % c.q);
             ra.full = full ? 1u : 0u;
-            const int r = launch_bs_repair_kernel(int(c.k), int(c.m), int(lost_int / c.q), ra, static_cast<hipStream_t>(stream));
+            // streaming variant (LDS-DMA, one workgroup per CU): auto when every CU gets a tile,
+            // always in exec mode "stream"
+            int nl = 0;
+            const int r = launch_bs_repair_kernel(int(c.k), int(c.m), int(lost_int / c.q), ra, static_cast<hipStream_t>(stream),
+                                                  dev, dev_props(dev).cus, xm == kExecStream ? 2 : 1, &nl);
             if (r < 0) return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: %s", hipGetErrorString(hipError_t(-r)));
             if (r > 0) {
-                t_last_launches++;
-                t_last_exec = "bs-repair";
+                t_last_launches += nl;
+                t_last_exec = r == 2 ? "bs-repair-stream" : "bs-repair";
                 return Error{};
             }
         }

@@ -21,6 +21,7 @@
 
 #include "bitslice.hpp"
 #include "kernels.hpp"
+#include "stream_encode.hpp"  // uniform_ptr
 
 namespace clay {
 namespace bs {
@@ -33,6 +34,7 @@ struct RepArgs {
     uint32_t full;         // 1: helper buffers are whole chunks (layer z at z * sc);
                            // 0: the beta plane layers in ascending order (layer j at j * sc)
     uint32_t ntiles, per_xcd;
+    uint64_t b_start;      // first byte position (k_bs_repair: tiles of [b_start, sc))
 };
 
 template <int Q>
@@ -254,6 +256,321 @@ struct BsRepair {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// k_bs_repair_stream -- the same algebra with the helpers streamed through LDS (the encode's
+// memory structure, stream_encode.hpp): one workgroup per CU, LOADERS dedicated waves issue every
+// LDS-DMA (global_load_lds_dwordx4 takes any byte alignment, so the 2 mod 8 rows of the BASELINE
+// (9,3,11) chunk stream like aligned ones) and do every counted vmcnt wait; compute waves read own
+// values and PRT companions from LDS instead of re-reading them through L1/L2 with unaligned
+// 16-byte loads.
+//
+//  * Tile = W = 32 * PARTS byte positions of every helper row; lane = (plane layer j, part) holds
+//    pieces part and part + PARTS of its row (32 positions, one bit-sliced dword per plane).
+//  * Node buffer = beta rows x W (padded to whole KiB: one DMA instruction fills 1 KiB), a ring
+//    of NB buffers.  Loads of a tile in step order: the real nodes of every section y != Y0
+//    (one step each: PRT + transpose + fold into the Q accumulators), then the nodes of section Y0
+//    other than the lost one (the output step, phase 3).
+//  * Row r's 16-byte piece k sits at slot k ^ swz(r) (PARTS = 8: odd rows swapped halves), so a
+//    wave's ds_read_b128 of own and companion rows are bank-conflict free.
+//  * The last tile of a sub-chunk may be partial (any length >= 16 bytes): its DMA reads a piece
+//    straddling the end from end - 16, the loader rewrites that piece in LDS byte by byte once it
+//    landed, and compute lanes store only the bytes inside the sub-chunk.
+// ---------------------------------------------------------------------------------------------
+struct RepStreamArgs {
+    RepArgs r;
+    uint32_t ntiles;   // tiles of W bytes (the last one partial if W does not divide sc)
+    uint32_t per_xcd;  // tiles per XCD region
+    uint32_t ns;       // workgroups per XCD
+};
+
+template <int KD, int M, int Y0, int PARTS, int LOADERS>
+struct BsRepairStream {
+    using B = BsRepair<KD, M, Y0>;
+    static constexpr int Q = B::Q, T = B::T, P = B::P, NI = B::NI;
+    static constexpr int W = 32 * PARTS, LANES = P * PARTS;
+    static constexpr int CWAVES = (LANES + 63) / 64;
+    static constexpr int BLOCK = 64 * (CWAVES + LOADERS);
+    static constexpr int NBLK = (P * W + 1023) / 1024;  // DMA instructions per node buffer
+    static constexpr int NODE = NBLK * 1024;
+    static constexpr int NB = (160 * 1024) / NODE;
+    static constexpr int LDS_BYTES = NB * NODE;
+    static constexpr int BPL = NBLK / LOADERS;  // blocks per loader wave per node
+    static_assert(NBLK % LOADERS == 0, "node blocks split evenly over the loader waves");
+    static_assert(PARTS == 8 || PARTS == 16, "piece swizzle derived for 8 / 16 parts");
+    static_assert(1024 % W == 0, "whole rows per DMA block");
+    static constexpr int RPB = 1024 / W;  // rows per DMA block
+
+    static constexpr bool real(int i) { return B::real(i); }
+    // sections in step order: y != Y0 ascending, then Y0
+    static constexpr int sec(int s) { return s < T - 1 ? (s < Y0 ? s : s + 1) : Y0; }
+    static constexpr int nreal(int y) {
+        int n = 0;
+        for (int x = 0; x < Q; x++) n += real(y * Q + x);
+        return n;
+    }
+    // first load of step s within a tile (the output step has nreal(Y0) - 1 loads)
+    static constexpr int soff(int s) {
+        int o = 0;
+        for (int i = 0; i < s && i < T - 1; i++) o += nreal(sec(i));
+        if (s >= T) o += nreal(Y0) - 1;
+        return o;
+    }
+    static constexpr int NT = soff(T);
+    static_assert(NB >= 2 * Q && NT >= 1, "ring: two steps' loads in flight");
+    __host__ __device__ static constexpr uint32_t swz(uint32_t r) { return PARTS == 8 ? (r & 1u) * 8u : 0u; }
+
+    // node of tile-relative load q (x0 = the lost node's x: skipped in section Y0)
+    __device__ static int node_of(int q, uint32_t x0) {
+        int n = 0;
+        for (int y = 0; y < T - 1; y++) {
+            const int yy = sec(y);
+            for (int x = 0; x < Q; x++)
+                if (real(yy * Q + x)) {
+                    if (n == q) return yy * Q + x;
+                    n++;
+                }
+        }
+        for (int x = 0; x < Q; x++)
+            if (real(Y0 * Q + x) && uint32_t(x) != x0) {
+                if (n == q) return Y0 * Q + x;
+                n++;
+            }
+        return -1;
+    }
+
+    // ---------------- loader ----------------
+    struct Loader {
+        uint32_t roff[BPL];  // row offset (layer * sc) of the lane's piece, per block of this wave
+        uint32_t k16[BPL];   // 16 * the piece index within the row
+    };
+    __device__ static void loader_init(Loader &L, const RepArgs &a, int li, int lane) {
+        const uint32_t x0 = a.x0;
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            const uint32_t blk = uint32_t(li * BPL + j);
+            uint32_t r = blk * uint32_t(RPB) + uint32_t(lane) * 16u / uint32_t(W);
+            const uint32_t slot = (uint32_t(lane) * 16u % uint32_t(W)) / 16u;
+            if (r >= uint32_t(P)) r = 0;  // padding of the last block: any valid row
+            const uint32_t l = a.full ? B::layer_of(r, x0) : r;
+            L.roff[j] = l * uint32_t(a.sc);
+            L.k16[j] = 16u * (slot ^ swz(r));
+        }
+    }
+    __device__ static void issue(const RepArgs &a, const Loader &L, uint32_t lds_buf, const uint8_t *node, uint32_t b0,
+                                 uint32_t vend, int li) {
+        lds_buf = __builtin_amdgcn_readfirstlane(lds_buf);
+        if (vend >= b0 + uint32_t(W)) {
+            const uint8_t *base = uniform_ptr(node + b0);
+#pragma unroll
+            for (int j = 0; j < BPL; j++) dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.roff[j] + L.k16[j]);
+        } else {
+            // partial tile (the last of the sub-chunk, vend = sc >= 16): a piece straddling vend
+            // is read from vend - 16 and rewritten by patch(), a piece wholly past it from b0
+            const uint8_t *base = uniform_ptr(node);
+#pragma unroll
+            for (int j = 0; j < BPL; j++) {
+                uint32_t pos = b0 + L.k16[j];
+                if (pos + 16u > vend) pos = pos >= vend ? b0 : vend - 16u;
+                dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.roff[j] + pos);
+            }
+        }
+    }
+    // after the partial tile's DMA landed: the piece holding vend, byte by byte (zero past it)
+    __device__ static void patch(const Loader &L, uint8_t *buf, const uint8_t *node, uint32_t b0, uint32_t vend, int li,
+                                 int lane) {
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            const uint32_t pos = b0 + L.k16[j];
+            if (pos < vend && pos + 16u > vend) {
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                const uint8_t *src = node + L.roff[j] + pos;
+                for (uint32_t b = 0; b < vend - pos; b++) w[b >> 2] |= uint32_t(src[b]) << (8u * (b & 3u));
+                *reinterpret_cast<uint4 *>(buf + (li * BPL + j) * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    }
+
+    // ---------------- compute ----------------
+    // 16 bytes v[w0 .. w0+3] at p, of which the first nv (<= 16) are inside the sub-chunk
+    __device__ static void store_part(uint8_t *p, const uint32_t (&v)[8], int w0, int nv) {
+        if (nv >= 16) {
+            *reinterpret_cast<uint4 *>(p) = make_uint4(v[w0], v[w0 + 1], v[w0 + 2], v[w0 + 3]);
+        } else {
+            for (int b = 0; b < nv; b++) p[b] = uint8_t(v[w0 + (b >> 2)] >> (8 * (b & 3)));
+        }
+    }
+    __device__ static void read32(const uint8_t *buf, uint32_t r, uint32_t part, uint32_t (&d)[8]) {
+        const uint8_t *row = buf + r * uint32_t(W);
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(row + ((part ^ swz(r)) << 4));
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(row + (((part + uint32_t(PARTS)) ^ swz(r)) << 4));
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+};
+
+// grid = 8 * ns workgroups (one per CU); XCD x owns full tiles [x * per_xcd, (x + 1) * per_xcd),
+// its ns workgroups take them round robin.
+// PROBE (bench_tools/repair_probe only; the library instantiates 0): bit 1 = compute waves skip
+// the math (garbage outputs), 2 = loaders issue no DMA, 4 = no output stores.
+template <int KD, int M, int Y0, int PARTS, int LOADERS, int PROBE = 0>
+__global__ __launch_bounds__((BsRepairStream<KD, M, Y0, PARTS, LOADERS>::BLOCK)) void k_bs_repair_stream(RepStreamArgs sa) {
+    using Kn = BsRepairStream<KD, M, Y0, PARTS, LOADERS>;
+    using B = typename Kn::B;
+    constexpr int Q = Kn::Q, T = Kn::T, NT = Kn::NT;
+    constexpr uint32_t NB = uint32_t(Kn::NB), NODE = uint32_t(Kn::NODE);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const RepArgs &a = sa.r;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, ns = sa.ns;
+    const uint32_t t0 = xcd * sa.per_xcd;
+    const uint32_t t1 = t0 + sa.per_xcd < sa.ntiles ? t0 + sa.per_xcd : sa.ntiles;
+    const uint32_t ntile = t0 + slot < t1 ? (t1 - t0 - slot + ns - 1) / ns : 0u;
+    const uint32_t x0 = a.x0;
+    if (ntile == 0) return;  // uniform per workgroup
+    const uint32_t sc32 = uint32_t(a.sc);
+    auto tile_b0 = [&](uint32_t k) { return (t0 + slot + k * ns) * uint32_t(Kn::W); };
+    auto tile_end = [&](uint32_t b0) { return b0 + uint32_t(Kn::W) < sc32 ? b0 + uint32_t(Kn::W) : sc32; };
+    const uint32_t nsteps = ntile * uint32_t(T);
+
+    if (wave >= Kn::CWAVES) {
+        // ---------------- loader waves ----------------
+        __builtin_amdgcn_s_setprio(3);
+        const int li = wave - Kn::CWAVES;
+        typename Kn::Loader L;
+        Kn::loader_init(L, a, li, lane);
+        const uint32_t lds0 = lds_addr_of(smem);
+        const uint32_t nloads = ntile * uint32_t(NT);
+        uint32_t issued = 0;
+        auto issue_upto = [&](uint32_t lim) {  // global load index limit
+            if (lim > nloads) lim = nloads;
+            for (; issued < lim; issued++) {
+                const uint32_t k = issued / uint32_t(NT), q = issued % uint32_t(NT);
+                const int nd = Kn::node_of(int(q), x0);
+                const uint32_t b0 = tile_b0(k);
+                if constexpr (!(PROBE & 2)) Kn::issue(a, L, lds0 + (issued % NB) * NODE, a.h[nd], b0, tile_end(b0), li);
+            }
+        };
+        issue_upto(NB);
+        for (uint32_t s = 0; s < nsteps; s++) {
+            const uint32_t k = s / uint32_t(T), st = s % uint32_t(T);
+            // loads of step s landed (everything issued after them may stay in flight)
+            const uint32_t qend = k * uint32_t(NT) + uint32_t(st + 1 < uint32_t(T) ? Kn::soff(int(st) + 1) : NT);
+            const uint32_t b0 = tile_b0(k), vend = tile_end(b0);
+            if (vend < b0 + uint32_t(Kn::W)) {
+                // partial tile: everything landed, then the straddling pieces of this step
+                wait_vm0();
+                if constexpr (!(PROBE & 2)) {
+                    for (uint32_t g = k * uint32_t(NT) + uint32_t(Kn::soff(int(st))); g < qend; g++) {
+                        const int nd = Kn::node_of(int(g % uint32_t(NT)), x0);
+                        Kn::patch(L, smem + (g % NB) * NODE, a.h[nd], b0, vend, li, lane);
+                    }
+                }
+            } else {
+                wait_vm_rt(int((issued - qend) * uint32_t(Kn::BPL)));
+            }
+            lds_barrier();
+            // steps before s are done: their buffers take the loads NB ahead
+            const uint32_t qs = k * uint32_t(NT) + uint32_t(Kn::soff(int(st)));
+            issue_upto(qs + NB);
+        }
+        wait_vm0();
+        return;
+    }
+
+    // ---------------- compute waves ----------------
+    const uint32_t j = uint32_t(threadIdx.x) / uint32_t(PARTS), part = uint32_t(threadIdx.x) % uint32_t(PARTS);
+    const bool active = j < uint32_t(Kn::P);
+    const uint32_t jr = active ? j : 0u;  // idle lanes of the last wave compute row 0, store nothing
+    uint32_t acc[Q * 8];
+    for (uint32_t k = 0; k < ntile; k++) {
+        const uint32_t b0 = tile_b0(k), vend = tile_end(b0);
+#pragma unroll
+        for (int w = 0; w < Q * 8; w++) acc[w] = 0;
+        sfor<T>([&](auto sc_) BS_INL {
+            constexpr int st = decltype(sc_)::value;
+            constexpr int Y = Kn::sec(st);
+            lds_barrier();  // step (k, st) landed
+            const uint32_t gq0 = k * uint32_t(NT) + uint32_t(Kn::soff(st));
+            if constexpr ((PROBE & 1) && st < T - 1) {
+                if (k == 0 && st == 0)
+#pragma unroll
+                    for (int w = 0; w < Q * 8; w++) acc[w] = (threadIdx.x * 0x9E3779B9u) ^ uint32_t(w);
+            } else if constexpr (st < T - 1) {
+                // fold section Y: U = PRT(own, companion) -> transpose -> RS solve rows
+                const uint32_t zy = (jr / B::jw(Y)) % uint32_t(Q);
+                constexpr uint32_t realY = [] {
+                    uint32_t m = 0;
+                    for (int x = 0; x < Q; x++) m |= uint32_t(B::real(Y * Q + x)) << x;
+                    return m;
+                }();
+                const bool creal = (realY >> zy) & 1u;
+                const uint32_t cq = gq0 + uint32_t(__builtin_popcount(realY & ((1u << zy) - 1u)));
+                const uint8_t *cbuf = smem + (cq % NB) * NODE;
+                sfor<Q>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    constexpr int I = Y * Q + X;
+                    constexpr int qx = __builtin_popcount(realY & ((1u << X) - 1u));
+                    uint32_t o[8], cv[8], u[8];
+                    if constexpr (B::real(I)) {
+                        Kn::read32(smem + ((gq0 + uint32_t(qx)) % NB) * NODE, jr, part, o);
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < 8; w++) o[w] = 0;
+                    }
+                    const uint32_t jc = jr + (uint32_t(X) - zy) * B::jw(Y);
+                    const bool keep = creal && zy != uint32_t(X);
+                    Kn::read32(creal ? cbuf : smem, creal ? jc : 0u, part, cv);
+                    const uint32_t km = keep ? 0xffffffffu : 0u;
+#pragma unroll
+                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4(o[w], cv[w] & km);
+                    transpose8(u);
+                    B::template fold<I>(u, acc);
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+            } else {
+                // output step: C(lost, z_j) = U(Y0, x0); C(lost, z_j[Y0 := x]) = gamma^-1 (U(Y0, x) + C(Y0, x))
+                const uint32_t zj = B::layer_of(jr, x0);
+                const uint64_t sc = a.sc;
+                sfor<Q>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    constexpr int I = Y0 * Q + X;
+                    uint32_t v[8];
+#pragma unroll
+                    for (int w = 0; w < 8; w++) v[w] = acc[X * 8 + w];
+                    transpose8(v);
+                    uint32_t z = zj;
+                    if (uint32_t(X) != x0) {
+                        if constexpr (B::real(I)) {
+                            // rank of X among section Y0's loaded nodes (real, != x0)
+                            uint32_t rk = 0;
+#pragma unroll
+                            for (int x = 0; x < X; x++) rk += (B::real(Y0 * Q + x) && uint32_t(x) != x0) ? 1u : 0u;
+                            uint32_t c[8];
+                            Kn::read32(smem + ((gq0 + rk) % NB) * NODE, jr, part, c);
+#pragma unroll
+                            for (int w = 0; w < 8; w++) v[w] ^= c[w];
+                        }
+                        constexpr GfTab tg = B::gamma_inv_tab();
+#pragma unroll
+                        for (int w = 0; w < 8; w++) v[w] = gf_mul(v[w], tg);
+                        z = zj + (uint32_t(X) - x0) * B::wt(Y0);
+                    }
+                    if (active && !(PROBE & 4)) {
+                        uint8_t *dst = a.out + uint64_t(z) * sc + b0;
+                        if (vend == b0 + uint32_t(Kn::W)) {
+                            *reinterpret_cast<uint4 *>(dst + 16u * part) = make_uint4(v[0], v[1], v[2], v[3]);
+                            *reinterpret_cast<uint4 *>(dst + 16u * (part + uint32_t(PARTS))) = make_uint4(v[4], v[5], v[6], v[7]);
+                        } else {
+                            Kn::store_part(dst + 16u * part, v, 0, int(vend - b0) - int(16u * part));
+                            Kn::store_part(dst + 16u * (part + uint32_t(PARTS)), v, 4, int(vend - b0) - int(16u * (part + uint32_t(PARTS))));
+                        }
+                    }
+                });
+            }
+        });
+    }
+}
+
 // grid = 8 * per_xcd blocks: XCD x streams tiles [x * per_xcd, (x + 1) * per_xcd)
 template <int KD, int M, int Y0>
 __global__ __launch_bounds__(256) void k_bs_repair(RepArgs a) {
@@ -262,7 +579,7 @@ __global__ __launch_bounds__(256) void k_bs_repair(RepArgs a) {
     const uint32_t tix = (blockIdx.x & 7u) * a.per_xcd + (blockIdx.x >> 3);
     if (tix >= a.ntiles) return;
     const uint32_t j = threadIdx.x / uint32_t(Kn::PARTS), part = threadIdx.x % uint32_t(Kn::PARTS);
-    const uint64_t b0 = uint64_t(tix) * Kn::W;
+    const uint64_t b0 = a.b_start + uint64_t(tix) * Kn::W;
     if (b0 + Kn::W <= a.sc) Kn::template tile<true>(a, j, part, b0);
     else Kn::template tile<false>(a, j, part, b0);
 }

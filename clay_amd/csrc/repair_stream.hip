@@ -1,42 +1,105 @@
-// repair_stream.hip -- instantiations and launcher of the bit-sliced repair kernel
+// repair_stream.hip -- instantiations and launchers of the bit-sliced repair kernels
 // (repair_kernel.hpp), in their own translation unit; the host-side checks are in engine.hip.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <set>
+#include <utility>
 
 #include "repair_kernel.hpp"
 
 namespace clay {
 
 template <int KD, int M, int Y0>
-static hipError_t launch_one(bs::RepArgs a, hipStream_t stream, uint32_t *w_out) {
+static hipError_t launch_one(bs::RepArgs a, hipStream_t stream) {
     using Kn = bs::BsRepair<KD, M, Y0>;
-    *w_out = Kn::W;
-    a.ntiles = uint32_t((a.sc + Kn::W - 1) / Kn::W);
+    a.ntiles = uint32_t((a.sc - a.b_start + Kn::W - 1) / Kn::W);
     a.per_xcd = (a.ntiles + 7) / 8;
     bs::k_bs_repair<KD, M, Y0><<<dim3(a.per_xcd * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
     return hipGetLastError();
 }
 
-template <int KD, int M>
-static hipError_t launch_km(int y0, const bs::RepArgs &a, hipStream_t stream, uint32_t *w) {
+// streaming variant: one workgroup per CU; returns hipErrorNotSupported when the launch should
+// fall back to the direct kernel
+template <int KD, int M, int Y0, int PARTS, int LOADERS>
+static hipError_t launch_stream(const bs::RepArgs &a, hipStream_t stream, int dev, int cus, bool force,
+                                int *launches, bool *streamed) {
+    using Kn = bs::BsRepairStream<KD, M, Y0, PARTS, LOADERS>;
+    const uint64_t nfull = a.sc / uint64_t(Kn::W);
+    const uint32_t ns = uint32_t(cus >= 8 ? cus / 8 : 1);
+    if (!force && nfull < uint64_t(8) * ns) return hipErrorNotSupported;  // under one tile per CU
+    if (a.sc < 16) return hipErrorNotSupported;  // a partial tile reads whole 16-byte pieces
+    if (a.sc * uint64_t(Kn::B::ALPHA) >= (uint64_t(1) << 32)) return hipErrorNotSupported;  // 32-bit row offsets
+    {
+        static std::mutex mu;
+        static std::set<int> done;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!done.count(dev)) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_bs_repair_stream<KD, M, Y0, PARTS, LOADERS>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
+            if (e != hipSuccess) return e;
+            done.insert(dev);
+        }
+    }
+    bs::RepStreamArgs sa{};
+    sa.r = a;
+    sa.ntiles = uint32_t((a.sc + Kn::W - 1) / Kn::W);
+    sa.per_xcd = (sa.ntiles + 7) / 8;
+    sa.ns = ns;
+    bs::k_bs_repair_stream<KD, M, Y0, PARTS, LOADERS><<<dim3(ns * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(sa);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    *launches += 1;
+    *streamed = true;
+    return hipSuccess;
+}
+
+template <int KD, int M, int PARTS, int LOADERS>
+static hipError_t launch_km(int y0, const bs::RepArgs &a, hipStream_t stream, int dev, int cus, int stream_mode,
+                            bool *streamed, int *launches) {
+    *streamed = false;
+    *launches = 1;
+    if constexpr (PARTS > 0) {
+        if (stream_mode > 0) {
+            *launches = 0;
+            hipError_t e = hipErrorNotSupported;
+            const bool force = stream_mode == 2;
+            switch (y0) {
+            case 0: e = launch_stream<KD, M, 0, PARTS, LOADERS>(a, stream, dev, cus, force, launches, streamed); break;
+            case 1: e = launch_stream<KD, M, 1, PARTS, LOADERS>(a, stream, dev, cus, force, launches, streamed); break;
+            case 2: e = launch_stream<KD, M, 2, PARTS, LOADERS>(a, stream, dev, cus, force, launches, streamed); break;
+            default:
+                if constexpr (bs::Shape<KD, M>::T > 3) e = launch_stream<KD, M, 3, PARTS, LOADERS>(a, stream, dev, cus, force, launches, streamed);
+                break;
+            }
+            if (e != hipErrorNotSupported) return e;
+            *launches = 1;
+        }
+    }
     switch (y0) {
-    case 0: return launch_one<KD, M, 0>(a, stream, w);
-    case 1: return launch_one<KD, M, 1>(a, stream, w);
-    case 2: return launch_one<KD, M, 2>(a, stream, w);
+    case 0: return launch_one<KD, M, 0>(a, stream);
+    case 1: return launch_one<KD, M, 1>(a, stream);
+    case 2: return launch_one<KD, M, 2>(a, stream);
     default:
-        if constexpr (bs::Shape<KD, M>::T > 3) return launch_one<KD, M, 3>(a, stream, w);
+        if constexpr (bs::Shape<KD, M>::T > 3) return launch_one<KD, M, 3>(a, stream);
         return hipErrorInvalidValue;
     }
 }
 
-// 1 = launched, 0 = no instantiation for (k, m), < 0 = HIP error
-int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream) {
-    uint32_t w = 0;
+// stream_mode: 0 = direct kernel, 1 = streaming kernel when the sub-chunk gives every CU a
+// tile, 2 = streaming kernel whenever the code has one.  Returns 1 = direct kernel launched,
+// 2 = streaming kernel launched, 0 = no instantiation for (k, m), < 0 = HIP error; *launches =
+// kernel launches issued (the streaming kernel adds one for a sub-chunk remainder).
+int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream, int dev, int cus,
+                            int stream_mode, int *launches) {
     hipError_t e;
-    if (k == 9 && m == 3) e = launch_km<9, 3>(y0, a, stream, &w);
-    else if (k == 10 && m == 4) e = launch_km<10, 4>(y0, a, stream, &w);
-    else if (k == 4 && m == 2) e = launch_km<4, 2>(y0, a, stream, &w);
+    bool streamed = false;
+    if (k == 9 && m == 3) e = launch_km<9, 3, 16, 7>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
+    else if (k == 10 && m == 4) e = launch_km<10, 4, 8, 4>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
+    else if (k == 4 && m == 2) e = launch_km<4, 2, 0, 0>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
     else return 0;
-    return e == hipSuccess ? 1 : -int(e);
+    if (e != hipSuccess) return -int(e);
+    return streamed ? 2 : 1;
 }
 
 }  // namespace clay

@@ -82,7 +82,8 @@ struct StreamMap {
     }
 };
 
-template <int KD, int LOADERS>
+// CPL / CPS: cache policy of the LDS-DMA loads / parity stores (0 default, 1 nt, 2 sc1)
+template <int KD, int LOADERS, int CPL = 0, int CPS = 0>
 struct StreamEnc {
     using K6 = Bs6Kernel<KD, 4, 8>;
     using S = typename K6::S;
@@ -150,7 +151,7 @@ struct StreamEnc {
                 if (full) {
                     const uint8_t *base = uniform_ptr(a.data[node] + (uint64_t(g) * sc + t.b0));
 #pragma unroll
-                    for (int j = 0; j < BPL; j++) dma16(dst + uint32_t(j) * 1024u, base, L.off[j]);
+                    for (int j = 0; j < BPL; j++) dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[j]);
                 } else {
                     // partial tile: a piece straddling vend is read from vend - 16 (patched
                     // after landing), a piece wholly past vend from b0 (never used)
@@ -158,7 +159,7 @@ struct StreamEnc {
                     uint32_t pos = t.b0 + L.k16;
                     if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
 #pragma unroll
-                    for (int j = 0; j < BPL; j++) dma16(dst + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
+                    for (int j = 0; j < BPL; j++) dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
                 }
             }
         });
@@ -302,8 +303,8 @@ struct StreamEnc {
             uint32_t off = (z - (odd ? 4u : 0u)) * uint32_t(a.sc);
             asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
             off += t.b0 + prel + (odd ? 128u : 0u);
-            st16s(a.par[X], off, lo[0], lo[1], lo[2], lo[3]);
-            st16s(a.par[X], off + 4u * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
+            st16sp<CPS>(a.par[X], off, lo[0], lo[1], lo[2], lo[3]);
+            st16sp<CPS>(a.par[X], off + 4u * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
         } else {
             uint8_t *p = a.par[X] + uint64_t(z) * a.sc + t.b0 + prel;
 #pragma unroll
@@ -364,12 +365,13 @@ struct StreamEnc {
 // XCD; grid = 8 * nslots; LDS = KD x 16 KiB (one workgroup per CU).
 // PROBE is for bench_tools/stream_probe.hip only (the library instantiates PROBE = 0):
 // bit 1 = compute waves skip the math, 2 = loaders skip the DMA, 4 = no parity stores,
+// 64/128 = LDS-DMA loads nt / sc1, 256/512 = parity stores nt / sc1,
 // 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1, 32 = the group whose
 // outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
 // across workgroups; only meaningful with bit 1).
 template <int KD, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
-    using Kn = StreamEnc<KD, LOADERS>;
+    using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3>;
     using K6 = typename Kn::K6;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;

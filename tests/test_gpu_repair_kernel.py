@@ -12,6 +12,15 @@ from clay_amd import ClayCode
 pytestmark = pytest.mark.gpu
 
 
+# codes with a streaming kernel (k_bs_repair_stream; exec mode "stream" runs it for sub-chunks of
+# at least 16 bytes, partial last tiles included)
+STREAM_CODES = {(9, 3, 11), (10, 4, 13)}
+
+
+def expect_path(cfg, sc):
+    return "bs-repair-stream" if cfg in STREAM_CODES and sc >= 16 else "bs-repair"
+
+
 @pytest.fixture
 def stream_exec():
     prev = clay_amd.set_exec_mode("stream")
@@ -20,7 +29,7 @@ def stream_exec():
 
 
 @pytest.mark.parametrize("cfg", [(9, 3, 11), (10, 4, 13), (4, 2, 5)])
-@pytest.mark.parametrize("sc", [2, 37, 288 + 2, 1000, 4096 + 6])
+@pytest.mark.parametrize("sc", [2, 16, 37, 288 + 2, 512, 1000, 4096 + 6])
 def test_bs_repair_every_node_random_helpers(oracle_mod, torch_cuda, stream_exec, cfg, sc):
     torch = torch_cuda
     c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
@@ -37,12 +46,12 @@ def test_bs_repair_every_node_random_helpers(oracle_mod, torch_cuda, stream_exec
         out = torch.full((chunk,), 0xA5, dtype=torch.uint8, device="cuda")
         c.repair_device(lost, helpers, [hb[i] for i in range(len(helpers))], chunk, out)
         torch.cuda.synchronize()
-        assert clay_amd.last_exec_path() == "bs-repair", clay_amd.last_exec_path()
+        assert clay_amd.last_exec_path() == expect_path(cfg, sc), clay_amd.last_exec_path()
         assert np.array_equal(out.cpu().numpy(), ref), (cfg, sc, lost, "gathered")
         out.fill_(0x5A)
         c.repair_device_full_chunks(lost, helpers, [fd[h] for h in helpers], chunk, out)
         torch.cuda.synchronize()
-        assert clay_amd.last_exec_path() == "bs-repair"
+        assert clay_amd.last_exec_path() == expect_path(cfg, sc)
         assert np.array_equal(out.cpu().numpy(), ref), (cfg, sc, lost, "full chunks")
 
 
@@ -64,11 +73,51 @@ def test_bs_repair_matches_grouped_executor(oracle_mod, torch_cuda):
             b = torch.empty(chunk, dtype=torch.uint8, device="cuda")
             clay_amd.set_exec_mode("stream")
             c.repair_device_full_chunks(lost, helpers, [full[h] for h in helpers], chunk, a)
-            assert clay_amd.last_exec_path() == "bs-repair"
+            assert clay_amd.last_exec_path() == "bs-repair-stream"
             clay_amd.set_exec_mode("grouped")
             c.repair_device_full_chunks(lost, helpers, [full[h] for h in helpers], chunk, b)
             assert clay_amd.last_exec_path() == "grouped"
             torch.cuda.synchronize()
             assert torch.equal(a, b), lost
+    finally:
+        clay_amd.set_exec_mode(prev)
+
+
+@pytest.mark.parametrize("cfg,sc", [((9, 3, 11), 512 * 256 * 3 + 37), ((10, 4, 13), 256 * 256 * 3 + 8)])
+def test_bs_repair_stream_many_tiles(oracle_mod, torch_cuda, cfg, sc):
+    """Several tiles per workgroup (the LDS ring wraps across tiles and within a tile) plus a
+    partial last tile: auto mode picks the streaming kernel; every lost node equals the grouped plan
+    executor (gathered helpers and whole chunks), two nodes are checked against the oracle."""
+    torch = torch_cuda
+    c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
+    chunk = c.sub_chunk_no * sc
+    full = torch.randint(0, 256, (c.n, chunk), dtype=torch.uint8, device="cuda")
+    prev = clay_amd.set_exec_mode("auto")
+    try:
+        for lost in range(c.n):
+            helpers = [i for i in range(c.n) if i != lost]
+            a = torch.full((chunk,), 0xA5, dtype=torch.uint8, device="cuda")
+            b = torch.full((chunk,), 0x5A, dtype=torch.uint8, device="cuda")
+            clay_amd.set_exec_mode("auto")
+            c.repair_device_full_chunks(lost, helpers, [full[h] for h in helpers], chunk, a)
+            assert clay_amd.last_exec_path() == "bs-repair-stream"
+            assert clay_amd.last_launch_count() == 1  # the partial last tile is in the same launch
+            clay_amd.set_exec_mode("grouped")
+            c.repair_device_full_chunks(lost, helpers, [full[h] for h in helpers], chunk, b)
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), (cfg, lost, "full chunks")
+            if lost in (0, c.n - 1):
+                info = c.minimum_to_repair(lost, helpers)
+                fh = full.cpu().numpy()
+                hd = {h: np.concatenate([fh[h][z * sc:(z + 1) * sc] for z in idx]) for h, idx in info}
+                ref = np.frombuffer(o.repair(lost, hd, chunk), dtype=np.uint8)
+                hb = torch.from_numpy(np.stack([hd[h] for h, _ in info])).cuda()
+                clay_amd.set_exec_mode("auto")
+                a.fill_(0)
+                c.repair_device(lost, [h for h, _ in info], [hb[i] for i in range(len(info))], chunk, a)
+                torch.cuda.synchronize()
+                assert clay_amd.last_exec_path() == "bs-repair-stream"
+                assert np.array_equal(a.cpu().numpy(), ref), (cfg, lost, "gathered vs oracle")
+                del hb
     finally:
         clay_amd.set_exec_mode(prev)

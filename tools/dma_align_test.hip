@@ -18,7 +18,7 @@ int main() {
     std::vector<uint8_t> h(4096); for (int i = 0; i < 4096; i++) h[i] = uint8_t(i * 7 + 3);
     uint8_t* d; uint32_t* o; hipMalloc(&d, 4096); hipMalloc(&o, 1024);
     hipMemcpy(d, h.data(), 4096, hipMemcpyHostToDevice);
-    for (int mis : {0, 4, 8, 12}) {
+    for (int mis : {0, 1, 2, 3, 4, 6, 8, 12}) {
         hipMemset(o, 0, 1024);
         k<<<1, 64, 1024>>>(d, o, mis);
         std::vector<uint8_t> r(1024); hipMemcpy(r.data(), o, 1024, hipMemcpyDeviceToHost);
