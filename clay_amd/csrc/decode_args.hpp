@@ -23,12 +23,16 @@ struct DecArgs {
     uint32_t sec_off[5];      // first load of section y's step within a tile
     uint32_t load_node[16];   // internal node of each load of a tile
     uint32_t nround;          // phase-B rounds
+    uint32_t round1;          // first round of iscore level >= 1 (split solve: level 0 is C = S')
     uint32_t round_start[24]; // first entry of each round in the layer order (+ end)
     // device buffer (kDecTabWords dwords), copied into LDS for phase B: v_perm tables of 8
     // dwords each (5 used) -- table t = r * 4 + j: row e_r of H_K^-1, check j; table
     // 16 + i * 4 + r: A_i[e_r] = (H_K^-1 gamma H_i)[e_r] for node i; then the phase-B layer
     // order (256 bytes) at dword kDecOrder
     const uint32_t *tabs;
+    // split mode (k_stream_syn + k_stream_solve): S of tile b0 / 64 at ws + (b0 / 64) * 64 KiB,
+    // layout [check j][layer z][64 B] (the S/C region of the fused kernel)
+    uint8_t *ws;
 };
 constexpr int kDecOrder = 640;
 constexpr int kDecTabWords = 768;  // 3 KiB: three 1 KiB LDS-DMA instructions

@@ -31,6 +31,37 @@ static hipError_t launch_one(const bs::DecArgs &a, hipStream_t stream, int dev) 
     return hipGetLastError();
 }
 
+template <int KD, int G, int SPROBE = 0, int SKIP = 0>
+static hipError_t launch_split(const bs::DecArgs &a, hipStream_t stream, int dev) {
+    using Kn = bs::StreamDec<KD, G>;
+    static std::mutex mu;
+    static std::set<int> done;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!done.count(dev)) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_syn<KD, G>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_solve<KD, G, SPROBE>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, bs::kSolveLds);
+            if (e != hipSuccess) return e;
+            done.insert(dev);
+        }
+    }
+    if (!(SKIP & 1)) {
+        bs::k_stream_syn<KD, G><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (SKIP & 2) return hipSuccess;
+    bs::DecArgs b = a;  // solve: 128-byte tiles, XCD regions of whole tiles, one workgroup per CU
+    const uint32_t nst = uint32_t((a.sc + 127) / 128);
+    b.region = (nst + 7) / 8 * 128;
+    bs::k_stream_solve<KD, G, SPROBE><<<dim3(b.nslots * 8), dim3(1024), bs::kSolveLds, stream>>>(b);
+    return hipGetLastError();
+}
+
+// a.ws != nullptr: split decode (two launches), else the fused single-launch kernel
 hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev) {
 #ifdef CLAY_DECODE_PROBES
     // CLAY_DECODE_PROBE: skip parts of the kernel (measurement only: the probe library
@@ -39,6 +70,17 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
         const char *e = getenv("CLAY_DECODE_PROBE");
         return e ? atoi(e) : 0;
     }();
+    if (kd == 10 && probe && a.ws) {
+        switch (probe) {  // split decode: 11 solve no work, 12 solve no stores, 13 syn only, 14 solve only,
+                          // 15 solve no S DMA
+        case 11: return launch_split<10, 3, 1>(a, stream, dev);
+        case 12: return launch_split<10, 3, 2>(a, stream, dev);
+        case 13: return launch_split<10, 3, 0, 2>(a, stream, dev);
+        case 14: return launch_split<10, 3, 0, 1>(a, stream, dev);
+        case 15: return launch_split<10, 3, 4>(a, stream, dev);
+        default: break;
+        }
+    }
     if (kd == 10 && probe) {
         switch (probe) {
         case 1: return launch_one<10, 3, 1>(a, stream, dev);
@@ -49,6 +91,11 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
         }
     }
 #endif
+    if (a.ws) {
+        if (kd == 10) return launch_split<10, 3>(a, stream, dev);
+        if (kd == 9) return launch_split<9, 3>(a, stream, dev);
+        return hipErrorInvalidValue;
+    }
     if (kd == 10) return launch_one<10, 3>(a, stream, dev);
     if (kd == 9) return launch_one<9, 3>(a, stream, dev);
     return hipErrorInvalidValue;

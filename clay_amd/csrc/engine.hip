@@ -1775,8 +1775,9 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
 hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
 
 template <int KD>
-static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
-                                  const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream, bool *done) {
+static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &prop, const uint8_t *const *cin,
+                                  uint8_t *const *cout, const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream,
+                                  bool *done) {
     *done = false;
     const clay_code_t &c = cs.code;
     using S = bs::Shape<KD, 4>;
@@ -1882,6 +1883,12 @@ static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uin
     }
     a.round_start[nr] = 256;
     a.nround = nr;
+    a.round1 = nr;
+    for (uint32_t r = 0; r < nr; r++)
+        if ((lay[a.round_start[r]].first >> 8) >= 1) {
+            a.round1 = r;
+            break;
+        }
     a.sc = sc;
     a.region = uint32_t(((sc + 7) / 8 + 63) / 64 * 64);
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
@@ -1899,9 +1906,19 @@ static Error launch_stream_decode(CodeState &cs, const DevProps &prop, const uin
         }
         a.tabs = it->second;
     }
+    // split decode (k_stream_syn + k_stream_solve, S through a pooled workspace of 64 KiB per
+    // 64-byte tile) unless CLAY_DECODE_SPLIT=0 selects the fused single-launch kernel
+    const char *sv = getenv("CLAY_DECODE_SPLIT");  // read per call: tests A/B both kernels
+    const bool split = !(sv && sv[0] == '0');
+    LeaseGuard ws(ds, stream);
+    if (split) {
+        Error le = lease_acquire(ds, (sc + 63) / 64 * 65536, stream, &ws.l);
+        if (le) return le;
+        a.ws = static_cast<uint8_t *>(ws.ptr());
+    }
     CLAY_HIP(launch_stream_decode_kernel(KD, a, stream, prop.dev));
-    t_last_launches++;
-    t_last_exec = "stream";
+    t_last_launches += split ? 2 : 1;
+    t_last_exec = split ? "stream-split" : "stream";
     *done = true;
     return Error{};
 }
@@ -1951,7 +1968,14 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         size_t in = internal_of(c, i);
         P.p[in] = chunks[i] ? const_cast<uint8_t *>(chunks[i]) : (want[in] ? outs[i] : nullptr);
     }
-    if (g_exec_mode.load(std::memory_order_relaxed) == kExecStream && tn == 16) {
+    // streaming decode (q = 4, t = 4 codes, one erasure per y-section, sc % 8 == 0): exec mode
+    // "stream" always; auto from 3 erasures on, where the split kernels beat the grouped plan
+    // executor ((10,4,13) 1 GiB: 4 erasures 0.77 vs 0.92 ms, 3: 0.72 vs 0.79; 2: 0.65 vs 0.57,
+    // 1: 0.59 vs 0.42 -- profiles/r03/decode_split/)
+    const int xmode = g_exec_mode.load(std::memory_order_relaxed);
+    size_t n_erased = 0;
+    for (size_t in = 0; in < tn; in++) n_erased += erased[in] && !(in >= c.k && in < c.k + c.nu) ? 1 : 0;
+    if ((xmode == kExecStream || (xmode == kExecAuto && n_erased >= 3)) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};
         for (size_t i = 0; i < c.n; i++) {
@@ -1962,8 +1986,8 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         bool done = false;
         const DevProps &prop = dev_props(dev);
         const size_t sc = chunk / c.sub_chunk_no;
-        if (c.k == 10) e = launch_stream_decode<10>(cs, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
-        else if (c.k == 9) e = launch_stream_decode<9>(cs, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
+        if (c.k == 10) e = launch_stream_decode<10>(cs, *ds, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
+        else if (c.k == 9) e = launch_stream_decode<9>(cs, *ds, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
         if (e || done) return e;
     }
     return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);

@@ -136,6 +136,8 @@ if __name__ == "__main__":
             ("decode", lambda: decode_cfg(4, 2, 5, 64 << 20, [0])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0])),
+            ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
+            ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 0)),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 11)),
             ("repair", lambda: repair_cfg(10, 4, 13, 107_374_592, 0)),

@@ -394,7 +394,10 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
 
 
 @pytest.mark.slow
-def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda):
+@pytest.mark.parametrize("mode,path", [("auto", "stream-split"), ("grouped", "grouped")])
+def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda, mode, path):
+    """BASELINE config 5 on random (non-codeword) chunks under the auto executor (the split
+    streaming decode) and the grouped plan executor."""
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     rng = np.random.default_rng(5)
@@ -406,9 +409,14 @@ def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda):
     ref = np.frombuffer(o.decode(av, er), np.uint8).reshape(10, chunk)
     full = torch.from_numpy(chunks).cuda()
     outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
-    c.decode_device([None if i in er else full[i] for i in range(14)], er,
-                    [outs[i] if i in er else None for i in range(14)], chunk)
-    torch.cuda.synchronize()
+    prev = clay_amd.set_exec_mode(mode)
+    try:
+        c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                        [outs[i] if i in er else None for i in range(14)], chunk)
+        torch.cuda.synchronize()
+        assert clay_amd.last_exec_path() == path
+    finally:
+        clay_amd.set_exec_mode(prev)
     for e in (0, 4, 8):
         assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
 
@@ -428,6 +436,7 @@ def test_cfg5_10_4_13_1GiB_decode_4_erasures_codeword_incl_parity(oracle_mod, to
     c.decode_device([None if i in er else full[i] for i in range(14)], er,
                     [outs[i] if i in er else None for i in range(14)], chunk)
     torch.cuda.synchronize()
+    assert clay_amd.last_exec_path() == "stream-split"  # auto, 4 erasures
     for e in er:
         assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
 

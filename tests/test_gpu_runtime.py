@@ -97,17 +97,18 @@ def test_host_api_concurrent_threads(oracle_mod, torch_cuda):
     assert not errors, errors
 
 
-def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda):
-    """Decodes on 8 distinct, short-lived streams one after another reuse the pooled U
-    workspace: the pool does not grow per stream (it grew by one workspace per stream
-    handle before the pool existed)."""
+@pytest.mark.parametrize("er,path", [([1, 5], "grouped"), ([0, 4, 8, 12], "stream-split")])
+def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path):
+    """Decodes on 8 distinct, short-lived streams one after another reuse the pooled
+    workspace (the grouped executor's U workspace, the split decode's S workspace): the pool
+    does not grow per stream (it grew by one workspace per stream handle before the pool
+    existed)."""
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     sc = 1024
     chunk = c.sub_chunk_no * sc
     ref = _stripe(o, 10, chunk, 99)
     full = torch.from_numpy(ref).cuda()
-    er = [1, 5]
     clay_amd.release_workspace(0)
     sizes = []
     for i in range(8):
@@ -116,11 +117,13 @@ def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda):
         c.decode_device([None if j in er else full[j] for j in range(14)], er,
                         [outs[j] if j in er else None for j in range(14)], chunk, 0, st.cuda_stream)
         st.synchronize()
+        assert clay_amd.last_exec_path() == path
         for e in er:
             assert np.array_equal(outs[e].cpu().numpy(), ref[e])
         sizes.append(clay_amd.workspace_bytes(0))
         del st
-    assert sizes[0] >= 16 * chunk  # one U workspace (q t = 16 nodes)
+    # one U workspace (q t = 16 nodes), or one S workspace (64 KiB per 64-byte tile)
+    assert sizes[0] >= (16 * chunk if path == "grouped" else (sc + 63) // 64 * 65536)
     assert sizes[-1] == sizes[0], sizes
     clay_amd.release_workspace(0)
     assert clay_amd.workspace_bytes(0) == 0

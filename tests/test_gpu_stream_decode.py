@@ -37,10 +37,13 @@ def _patterns(c, seed, n3, n4):
     return pats
 
 
-@pytest.fixture
-def auto_exec():
+@pytest.fixture(params=["split", "fused"])
+def auto_exec(request, monkeypatch):
+    """exec mode "stream": the split decode (k_stream_syn + k_stream_solve, default) or the fused
+    single-launch kernel (CLAY_DECODE_SPLIT=0); yields the path name last_exec_path() reports."""
+    monkeypatch.setenv("CLAY_DECODE_SPLIT", "1" if request.param == "split" else "0")
     prev = clay_amd.set_exec_mode("stream")
-    yield
+    yield "stream-split" if request.param == "split" else "stream"
     clay_amd.set_exec_mode(prev)
 
 
@@ -78,7 +81,7 @@ def test_stream_decode_patterns_random_inputs(oracle_mod, torch_cuda, auto_exec,
         got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
         path = clay_amd.last_exec_path()
         if stream_eligible(c, er):
-            assert path == "stream", (er, path)
+            assert path == auto_exec, (er, path)
             n_stream += 1
         ref = _oracle_erased(o, c, chunks, er)
         for e in er:
@@ -103,12 +106,12 @@ def test_stream_decode_codeword_incl_parity(oracle_mod, torch_cuda, auto_exec, c
     pats += [p for p in _patterns(c, 5, 12, 12) if stream_eligible(c, p)]
     for er in pats:
         got = _decode_dev(torch, c, ref, er, chunk)
-        assert clay_amd.last_exec_path() == "stream", er
+        assert clay_amd.last_exec_path() == auto_exec, er
         for e in er:
             assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e)
 
 
-def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda):
+def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, auto_exec):
     """Same random inputs through the streaming kernel (auto) and the grouped plan executor:
     identical bytes, including the rebuilt parity chunk."""
     torch = torch_cuda
@@ -117,14 +120,11 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda):
     chunk = c.sub_chunk_no * sc
     chunks = np.random.default_rng(9).integers(0, 256, (c.n, chunk), dtype=np.uint8)
     er = [1, 6, 9, 13]
-    prev = clay_amd.set_exec_mode("stream")
-    try:
-        a = _decode_dev(torch, c, chunks, er, chunk)
-        assert clay_amd.last_exec_path() == "stream"
-        clay_amd.set_exec_mode("grouped")
-        b = _decode_dev(torch, c, chunks, er, chunk)
-        assert clay_amd.last_exec_path() == "grouped"
-    finally:
-        clay_amd.set_exec_mode(prev)
+    a = _decode_dev(torch, c, chunks, er, chunk)
+    assert clay_amd.last_exec_path() == auto_exec
+    clay_amd.set_exec_mode("grouped")
+    b = _decode_dev(torch, c, chunks, er, chunk)
+    assert clay_amd.last_exec_path() == "grouped"
+    clay_amd.set_exec_mode("stream")
     for e in er:
         assert np.array_equal(a[e], b[e]), e
