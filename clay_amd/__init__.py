@@ -114,9 +114,11 @@ _EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3}
 
 def set_exec_mode(mode: str) -> str:
     """Process-wide plan executor for decode / repair / staged encode: 'auto' (tile-fused
-    where the U slots fit in LDS, else grouped), 'grouped' (one launch per level) or
-    'tile', or 'stream' (the single-launch streaming decode for q = 4, t = 4 codes where
-    eligible, else as auto).  Every mode produces the reference's bytes.  Returns the previous mode."""
+    where the U slots fit in LDS, else grouped; the split streaming decode for >= 3 erasures of
+    q = 4, t = 4 codes; the bit-sliced repair kernels for q = m repairs from all n - 1 nodes),
+    'grouped' (one launch per level), 'tile', or 'stream' (the split streaming decode for every
+    eligible q = 4, t = 4 decode -- CLAY_DECODE_SPLIT=0: the fused single-launch kernel -- else
+    as auto).  Every mode produces the reference's bytes.  Returns the previous mode."""
     if mode not in _EXEC_MODES:
         raise ValueError(f"unknown exec mode {mode!r}")
     prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])
@@ -124,7 +126,8 @@ def set_exec_mode(mode: str) -> str:
 
 
 def last_exec_path() -> str:
-    """Plan executor of this thread's last decode / repair / staged encode: 'tile' | 'grouped'."""
+    """Plan executor of this thread's last decode / repair / staged encode: 'tile' | 'grouped' |
+    'stream-split' | 'stream' | 'bs-repair-stream' | 'bs-repair' | 'none'."""
     return _lib.lib().clay_last_exec_path().decode()
 
 

@@ -24,6 +24,7 @@ struct DecArgs {
     uint32_t load_node[16];   // internal node of each load of a tile
     uint32_t nround;          // phase-B rounds
     uint32_t round1;          // first round of iscore level >= 1 (split solve: level 0 is C = S')
+    uint32_t pstart[25];      // split solve: correction pairs of round r at [pstart[r], pstart[r+1])
     uint32_t round_start[24]; // first entry of each round in the layer order (+ end)
     // device buffer (kDecTabWords dwords), copied into LDS for phase B: v_perm tables of 8
     // dwords each (5 used) -- table t = r * 4 + j: row e_r of H_K^-1, check j; table
@@ -35,7 +36,11 @@ struct DecArgs {
     uint8_t *ws;
 };
 constexpr int kDecOrder = 640;
-constexpr int kDecTabWords = 768;  // 3 KiB: three 1 KiB LDS-DMA instructions
+// split solve: correction pairs (uint16 layer | Y << 8 | X << 10: C(e_Y, z[Y:=X]) feeds layer z)
+// from dword kDecPairs; at most 768 (4 erasures: 108 x 3 + 54 x 6 + 12 x 9 + 12)
+constexpr int kDecPairs = 704;
+constexpr int kDecMaxPairs = 1152;
+constexpr int kDecTabWords = 1280;  // 5 KiB: 1 KiB LDS-DMA instructions (the fused kernel copies the first 3)
 
 }  // namespace bs
 }  // namespace clay

@@ -78,6 +78,8 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
         case 13: return launch_split<10, 3, 0, 2>(a, stream, dev);
         case 14: return launch_split<10, 3, 0, 1>(a, stream, dev);
         case 15: return launch_split<10, 3, 4>(a, stream, dev);
+        case 16: return launch_split<10, 3, 8, 1>(a, stream, dev);   // solve only, no presolve
+        case 17: return launch_split<10, 3, 16, 1>(a, stream, dev);  // solve only, no rounds
         default: break;
         }
     }

@@ -1889,6 +1889,28 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
             a.round1 = r;
             break;
         }
+    // split solve: the dropped terms of every round as (layer, section Y, node X) pairs
+    {
+        uint16_t *pairs = reinterpret_cast<uint16_t *>(&tabs[bs::kDecPairs]);
+        uint32_t np = 0;
+        for (uint32_t r = 0; r < nr; r++) {
+            a.pstart[r] = np;
+            if (r < a.round1) continue;
+            for (uint32_t li = a.round_start[r]; li < a.round_start[r + 1]; li++) {
+                const uint32_t z = ord[li];
+                for (int y = 0; y < 4; y++) {
+                    const uint32_t xe = (z >> (2 * (3 - y))) & 3u;
+                    if (!((a.emask[y] >> xe) & 1u)) continue;  // section y not red in z
+                    for (uint32_t x = 0; x < 4; x++) {
+                        if (x == xe || !((used >> (4 * y + x)) & 1u)) continue;
+                        if (np >= uint32_t(bs::kDecMaxPairs)) return Error{};
+                        pairs[np++] = uint16_t(z | uint32_t(y) << 8 | x << 10);
+                    }
+                }
+            }
+        }
+        a.pstart[nr] = np;
+    }
     a.sc = sc;
     a.region = uint32_t(((sc + 7) / 8 + 63) / 64 * 64);
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));

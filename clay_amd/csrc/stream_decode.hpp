@@ -472,6 +472,35 @@ struct StreamDec {
         }
         lds_barrier();  // every C of the tile in LDS
     }
+    // rounds3: the same corrections, one work item per (pair, dword): the pair's term
+    // A_(Y,X)[r] C(e_Y, z[Y:=X]) of one dword for every r, XORed into C_r(z) with LDS atomics.
+    // A round's latency is then its item count / 1024 instead of its layers' term count.
+    __device__ static void rounds3(const DecArgs &a, uint8_t *scb0, const uint8_t *tl, uint32_t tid) {
+        const uint32_t nround = a.nround;
+        const uint16_t *pairs = reinterpret_cast<const uint16_t *>(tl + kDecPairs * 4);
+        for (uint32_t rd = a.round1; rd < nround; rd++) {
+            lds_barrier();  // C of the previous round visible
+            const uint32_t i0 = a.pstart[rd] * 32u, i1 = a.pstart[rd + 1] * 32u;
+            for (uint32_t i = i0 + tid; i < i1; i += 1024u) {
+                const uint32_t pr = pairs[i >> 5], d4 = (i & 31u) * 4u;
+                const uint32_t z = pr & 255u, Y = (pr >> 8) & 3u, X = pr >> 10;
+                const uint32_t sh = 2u * (3u - Y), zy = (z >> sh) & 3u;
+                const uint32_t zs = z + ((X - zy) << sh);  // z[Y := X]
+                const int ry = a.rix[4 * Y + zy];           // the erased node of section Y (red in z)
+                const uint32_t cv = *reinterpret_cast<const uint32_t *>(scb0 + uint32_t(ry) * SBUF + zs * SW + d4);
+                const GfIdx ix = gf_idx(cv);
+                const uint8_t *tb = tl + (16u + (Y * 4u + X) * 4u) * 32u;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    if (uint32_t(r) >= a.ne) break;
+                    const GfTab t = tab_at(tb, r);
+                    __hip_atomic_fetch_xor(reinterpret_cast<uint32_t *>(scb0 + r * SBUF + z * SW + d4), gf_mul_idx(ix, t),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        lds_barrier();  // every C of the tile in LDS
+    }
     // C of the tile to the output chunks: 8 lanes x 16 bytes per 128-byte row
     template <bool STORE>
     __device__ static void store_out(const DecArgs &a, const uint8_t *scb0, int r, uint32_t b0, uint32_t vend, uint32_t tid) {
@@ -684,10 +713,10 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_syn(DecArg
     }
 }
 
-constexpr int kSolveLds = 4 * 256 * 128 + 3072;  // S/C tile (128 positions) + tables and layer order
+constexpr int kSolveLds = 4 * 256 * 128 + kDecTabWords * 4;  // S/C tile (128 positions) + tables, order, pairs
 
 // PROBE (CLAY_DECODE_PROBE, probe library only): bit 1 = no presolve / rounds, 2 = no HBM
-// stores, 4 = no S DMA.  grid = 8 * ns (one 1024-thread workgroup per CU); XCD x owns 128-byte
+// stores, 4 = no S DMA, 8 = no presolve, 16 = no rounds.  grid = 8 * ns (one 1024-thread workgroup per CU); XCD x owns 128-byte
 // tiles [x * per, (x + 1) * per) (a.region = per * 128), its ns workgroups take them round robin.
 template <int KD, int G, int PROBE = 0>
 __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
@@ -703,7 +732,7 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
     if (ntile == 0) return;  // uniform per workgroup
     const uint32_t lds0 = lds_addr_of(smem);
     uint8_t *const tl = smem + 4 * Kn::SBUF;
-    if (wave < 3)  // tables + layer order: 3 KiB, once per workgroup
+    if (wave < kDecTabWords / 256)  // tables, layer order, correction pairs: once per workgroup
         dma16(lds0 + 4u * Kn::SBUF + uint32_t(wave) * 1024u, uniform_ptr(reinterpret_cast<const uint8_t *>(a.tabs)),
               uint32_t(wave) * 1024u + uint32_t(lane) * 16u);
     const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
@@ -725,24 +754,51 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
     auto tile_b0 = [&](uint32_t k) { return (t0 + wslot + k * ns) * SW; };
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) dma_check(tile_b0(0), j);
+    // output stores of a full tile per lane (issued after the next tile's DMA, so the wait for
+    // that DMA lets them stay in flight): 2 per erased index with an output
+    uint32_t nstores = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) nstores += (uint32_t(r) < a.ne && a.out[r]) ? 2u : 0u;
     for (uint32_t k = 0; k < ntile; k++) {
         const uint32_t b0 = tile_b0(k);
         const uint32_t vend = b0 + SW < sc ? b0 + SW : sc;
-        wait_vm0();
+        if (k == 0) wait_vm0();                 // S of tile 0 and the tables
+        else wait_vm_rt(PROBE & 2 ? 0 : int(nstores));  // S of tile k (tile k-1's stores may stay in flight)
         lds_barrier();  // S (and, first time, the tables) landed
         if constexpr (!(PROBE & 1)) {
-            Kn::presolve(smem, tl, c0, p);
-            Kn::rounds2(a, smem, tl, c0, p);  // ends with a barrier
+            if constexpr (!(PROBE & 8)) Kn::presolve(smem, tl, c0, p);
+            if constexpr (!(PROBE & 16)) Kn::rounds3(a, smem, tl, threadIdx.x);  // ends with a barrier
+            else lds_barrier();
         } else {
             lds_barrier();
         }
-        // C of erased index r out, then buffer r takes check r of the next tile: the DMA streams
-        // behind the stores instead of after them
+        // C of the tile into registers (32 VGPRs: the rounds' registers are free by now), the
+        // next tile's S DMA into the freed region, then the output stores from registers
+        uint4 cv[4][2];
+        const uint32_t q16 = (threadIdx.x & 7u) * 16u;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            Kn::template store_out<!(PROBE & 2)>(a, smem, r, b0, vend, threadIdx.x);
-            lds_barrier();  // buffer r read by every wave
-            if (k + 1 < ntile) dma_check(tile_b0(k + 1), uint32_t(r));
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (uint32_t zz = 0; zz < 2; zz++)
+                cv[r][zz] = *reinterpret_cast<const uint4 *>(smem + r * Kn::SBUF + ((threadIdx.x >> 3) + 128u * zz) * SW + q16);
+        lds_barrier();  // the region is free
+        if (k + 1 < ntile)
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) dma_check(tile_b0(k + 1), j);
+        if constexpr (!(PROBE & 2)) {
+            const bool full = b0 + q16 + 16u <= vend;
+            const bool half = !full && b0 + q16 + 8u <= vend;  // sc % 8 == 0: valid length is a multiple of 8
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                uint8_t *dst = a.out[r];
+                if (uint32_t(r) >= a.ne || !dst) continue;
+#pragma unroll
+                for (uint32_t zz = 0; zz < 2; zz++) {
+                    uint8_t *o = dst + uint64_t((threadIdx.x >> 3) + 128u * zz) * sc + b0 + q16;
+                    if (full) *reinterpret_cast<uint4 *>(o) = cv[r][zz];
+                    else if (half) *reinterpret_cast<uint2 *>(o) = make_uint2(cv[r][zz].x, cv[r][zz].y);
+                }
+            }
         }
     }
 }

@@ -253,19 +253,26 @@ int clay_set_encode_path(int mode);
  * reference counterpart -- the crate has one CPU path):
  *   0 auto    -- the tile-fused executor (one launch, U workspace in LDS) for small plans
  *                (<= 32 op groups) whose U slots fit the LDS budget, else the grouped
- *                per-level executor
+ *                per-level executor; decodes of >= 3 erasures of q = 4, t = 4 codes
+ *                ((10,4,13), (9,4,12)) in distinct y-sections with sc % 8 == 0, sc >= 512 run
+ *                the split streaming decode (k_stream_syn + k_stream_solve, last path
+ *                "stream-split")
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
  *   (auto and stream: repair of (9,3,11), (10,4,13), (4,2,5) from all n - 1 other nodes runs
- *    the bit-sliced repair kernel k_bs_repair, last path "bs-repair")
- *   3 stream  -- decode of q = 4, t = 4 codes ((10,4,13), (9,4,12)) on the single-launch
- *                streaming decode kernel when the erasures sit in distinct y-sections and
- *                sc % 8 == 0, sc >= 512 (last path "stream"); everything else as auto
+ *    the bit-sliced repair kernels: k_bs_repair_stream (LDS-DMA streaming, one workgroup per
+ *    CU; auto when the sub-chunk gives every CU a tile, stream for any sub-chunk >= 16 bytes
+ *    of (9,3,11) / (10,4,13); last path "bs-repair-stream"), else k_bs_repair ("bs-repair"))
+ *   3 stream  -- every eligible decode of q = 4, t = 4 codes (any erasure count) on the split
+ *                streaming decode ("stream-split"; with the environment variable
+ *                CLAY_DECODE_SPLIT=0 the fused single-launch k_stream_decode, "stream");
+ *                everything else as auto
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
  * unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
- * "tile" (k_texec), "grouped" (k_gexec), "stream" (k_stream_decode), "bs-repair"
+ * "tile" (k_texec), "grouped" (k_gexec), "stream-split" (k_stream_syn + k_stream_solve),
+ * "stream" (k_stream_decode), "bs-repair-stream" (k_bs_repair_stream), "bs-repair"
  * (k_bs_repair) or "none". */
 const char *clay_last_exec_path(void);
 
