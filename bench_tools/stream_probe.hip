@@ -63,6 +63,18 @@ int main(int argc, char **argv) {
     };
     for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
     (void)hipDeviceSynchronize();
+    if (argc > 2 && argv[2][0] == 'x') {  // CSE folds A/B (PROBE bit 1024 = without)
+        printf("sc %u cse folds\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("L4 full, row-by-row folds", run<4, 1024>(a, 15));
+            rep("L4 full (CSE folds)", run<4, 0>(a, 15));
+            rep("L0 full, row-by-row folds", run<0, 1024>(a, 15));
+            rep("L0 full (CSE folds)", run<0, 0>(a, 15));
+            rep("L4 math + stores, row-by-row folds", run<4, 1026>(a, 15));
+            rep("L4 math + stores (CSE folds)", run<4, 2>(a, 15));
+        }
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'c') {  // cache-policy A/B (PROBE bits 64..512)
         printf("sc %u cache policies\n", sc);
         for (int rr = 0; rr < 2; rr++) {

@@ -22,6 +22,7 @@
 #pragma once
 
 #include "bitslice.hpp"
+#include "xor_cse.hpp"
 
 namespace clay {
 namespace bs {
@@ -335,6 +336,23 @@ struct Bs6Kernel {
         const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
 #pragma unroll
         for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+    }
+    // the fold's 32 output rows for node (Y, X), CSE-factored at compile time (xor_cse.hpp)
+    template <int Y, int X>
+    struct FoldCse {
+        static constexpr XorCse make() {
+            uint32_t rows[Q * 8] = {};
+            for (int p = 0; p < Q; p++)
+                for (int bo = 0; bo < 8; bo++) rows[p * 8 + bo] = uint32_t(plane_mask(S::RS.g[p][Y * Q + X], bo, 0));
+            return make_xor_cse(rows);
+        }
+        static constexpr XorCse C = make();
+    };
+    // bit transpose + RS fold of U[x] into the accumulators, through the CSE temporaries
+    template <int Y, int X>
+    __device__ static void fold_x_cse(uint32_t (&u)[8], uint32_t (&acc)[Q * 8]) {
+        transpose8(u);
+        cse_fold<FoldCse<Y, X>, Q * 8, (Y > 0 || X > 0)>(u, acc);
     }
     // bit transpose + RS fold of U[x] into the accumulators.
     template <int Y, int X>

@@ -119,6 +119,9 @@ struct BsRepair {
         return z;
     }
 
+    // acc (section Y0's q U values, 8 planes each) ^= R(., I) * u.  Row by row: the CSE form
+    // (xor_cse.hpp) needs temporaries that push the streaming kernel (14 waves, 128 VGPRs) into
+    // spills, and the kernel is memory-bound anyway.
     template <int I>
     __device__ static void fold(uint32_t (&u)[8], uint32_t (&acc)[Q * 8]) {
         sfor<Q>([&](auto xc) BS_INL {

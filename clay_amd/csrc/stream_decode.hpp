@@ -42,6 +42,7 @@
 #include "decode_args.hpp"
 #include "kernels.hpp"
 #include "stream_encode.hpp"  // uniform_ptr, bit-slice helpers
+#include "xor_cse.hpp"
 
 namespace clay {
 namespace bs {
@@ -109,20 +110,23 @@ struct StreamDec {
             *reinterpret_cast<uint2 *>(buf + (b + ((uint32_t(g) ^ cl) << 6))) = make_uint2(d[2 * g], d[2 * g + 1]);
     }
 
-    // S[p] (8 planes) ^= f * H(p, I) * u, f = gamma if GAMMA
+    // S[p] (8 planes) ^= f * H(p, I) * u, f = gamma if GAMMA; through compile-time common
+    // subexpressions of the 32 rows (xor_cse.hpp)
+    template <int I, bool GAMMA>
+    struct FoldCse {
+        static constexpr XorCse make() {
+            uint32_t rows[32] = {};
+            for (int p = 0; p < 4; p++) {
+                const uint8_t h = GAMMA ? gm(2, H(p, I)) : H(p, I);
+                for (int bo = 0; bo < 8; bo++) rows[p * 8 + bo] = uint32_t(plane_mask(h, bo, 0));
+            }
+            return make_xor_cse(rows);
+        }
+        static constexpr XorCse C = make();
+    };
     template <int I, bool GAMMA>
     __device__ static void fold(const uint32_t (&u)[8], uint32_t (&s)[32]) {
-        sfor<4>([&](auto pc) BS_INL {
-            constexpr int p = decltype(pc)::value;
-            constexpr uint8_t h = GAMMA ? gm(2, H(p, I)) : H(p, I);
-            if constexpr (h != 0) {
-                sfor<8>([&](auto bc) BS_INL {
-                    constexpr int bo = decltype(bc)::value;
-                    constexpr uint64_t mk = plane_mask(h, bo, 0);
-                    s[p * 8 + bo] = xor_sel<mk, true>(s[p * 8 + bo], u);
-                });
-            }
-        });
+        cse_fold<FoldCse<I, GAMMA>, 32, true>(u, s);
     }
 
     // ---------------- tile map ----------------

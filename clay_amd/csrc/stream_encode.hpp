@@ -82,8 +82,9 @@ struct StreamMap {
     }
 };
 
-// CPL / CPS: cache policy of the LDS-DMA loads / parity stores (0 default, 1 nt, 2 sc1)
-template <int KD, int LOADERS, int CPL = 0, int CPS = 0>
+// CPL / CPS: cache policy of the LDS-DMA loads / parity stores (0 default, 1 nt, 2 sc1);
+// CSE: RS folds through compile-time common subexpressions (xor_cse.hpp)
+template <int KD, int LOADERS, int CPL = 0, int CPS = 0, bool CSE = true>
 struct StreamEnc {
     using K6 = Bs6Kernel<KD, 4, 8>;
     using S = typename K6::S;
@@ -276,7 +277,8 @@ struct StreamEnc {
             if constexpr (x + 1 < Q) load_x<Y, x + 1>(slot, L, o[(x + 1) & 1], cv[(x + 1) & 1]);
             uint32_t u[8];
             prt_x<Y, x>(o[x & 1], cv[x & 1], L, u);
-            K6::template fold_x<Y, x>(u, acc);
+            if constexpr (CSE) K6::template fold_x_cse<Y, x>(u, acc);
+            else K6::template fold_x<Y, x>(u, acc);
             __builtin_amdgcn_sched_barrier(0);
         });
     }
@@ -365,13 +367,14 @@ struct StreamEnc {
 // XCD; grid = 8 * nslots; LDS = KD x 16 KiB (one workgroup per CU).
 // PROBE is for bench_tools/stream_probe.hip only (the library instantiates PROBE = 0):
 // bit 1 = compute waves skip the math, 2 = loaders skip the DMA, 4 = no parity stores,
-// 64/128 = LDS-DMA loads nt / sc1, 256/512 = parity stores nt / sc1,
+// 64/128 = LDS-DMA loads nt / sc1, 256/512 = parity stores nt / sc1, 1024 = row-by-row folds
+// (no CSE: bench_tools/stream_probe x, 0.350 vs 0.353 ms full, 0.257 vs 0.281 math + stores),
 // 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1, 32 = the group whose
 // outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
 // across workgroups; only meaningful with bit 1).
 template <int KD, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
-    using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3>;
+    using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3, ((PROBE >> 10) & 1) == 0>;
     using K6 = typename Kn::K6;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
