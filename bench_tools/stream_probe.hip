@@ -36,6 +36,28 @@ static float run(BsArgs a, int reps) {
     return t[t.size() / 2];
 }
 
+// steady state: n back-to-back launches between one pair of events (what bench.py and the
+// profiler see); mean per launch
+template <int L, int PROBE>
+static float run_b2b(BsArgs a, int n) {
+    using Kn = StreamEnc<10, L>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_stream_encode<10, L, PROBE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int i = 0; i < 50; i++)
+        k_stream_encode<10, L, PROBE><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < n; i++)
+        k_stream_encode<10, L, PROBE><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / float(n);
+}
+
 int main(int argc, char **argv) {
     // sc of the BASELINE stripe by default; another value (e.g. 419456 = 128-aligned rows)
     // isolates the cost of the 8-byte row alignment of the reference layout
@@ -63,6 +85,16 @@ int main(int argc, char **argv) {
     };
     for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
     (void)hipDeviceSynchronize();
+    if (argc > 2 && argv[2][0] == 'b') {  // steady state, back-to-back launches
+        printf("sc %u back-to-back (200 launches after 50 untimed)\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b L4 full (CSE)", run_b2b<4, 0>(a, 200));
+            rep("b2b L4 full, no CSE", run_b2b<4, 1024>(a, 200));
+            rep("b2b L4 memory only", run_b2b<4, 1>(a, 200));
+            rep("b2b L4 math + stores (CSE)", run_b2b<4, 2>(a, 200));
+        }
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'x') {  // CSE folds A/B (PROBE bit 1024 = without)
         printf("sc %u cse folds\n", sc);
         for (int rr = 0; rr < 3; rr++) {

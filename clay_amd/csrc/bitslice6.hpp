@@ -401,6 +401,34 @@ struct Bs6Kernel {
                 if (i < nv) *reinterpret_cast<uint2 *>(p + 8 * i) = make_uint2(cv[2 * i], cv[2 * i + 1]);
         }
     }
+    // both PFT outputs of a pair at once: c[0..7] = pft(u, us), c[8..15] = pft(us, u), the 16
+    // rows over the 16 input planes factored by xor_cse.hpp (60 -> ~20 XOR instructions)
+    struct PftCse {
+        static constexpr XorCse make() {
+            uint32_t rows[16] = {};
+            for (int bo = 0; bo < 8; bo++) {
+                rows[bo] = uint32_t(pft_mask_of(bo, 0));
+                rows[8 + bo] = uint32_t(pft_mask_of(bo, 8));
+            }
+            return make_xor_cse<16, 16>(rows);
+        }
+        static constexpr XorCse C = make();
+    };
+    // mask of output plane bo of pft(first, second) over (u at bits 0-7, us at 8-15); base 8:
+    // the swapped pair pft(us, u)
+    static constexpr uint64_t pft_mask_of(int bo, int base) {
+        return base == 0 ? (plane_mask(S::DINV, bo, 0) | plane_mask(gm(S::DINV, 2), bo, 8))
+                         : (plane_mask(S::DINV, bo, 8) | plane_mask(gm(S::DINV, 2), bo, 0));
+    }
+    __device__ static void pft_pair(const uint32_t *u, const uint32_t *us, uint32_t (&c)[16]) {
+        uint32_t in[16];
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            in[w] = u[w];
+            in[8 + w] = us[w];
+        }
+        cse_fold<PftCse, 16, false, 16>(in, c);
+    }
     // PFT pair: C = det^-1 (u + gamma * ustar)
     __device__ static void pft(const uint32_t *u, const uint32_t *us, uint32_t (&cv)[8]) {
         uint32_t in[16];

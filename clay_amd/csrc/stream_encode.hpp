@@ -333,11 +333,27 @@ struct StreamEnc {
         auto pair = [&](const uint32_t *uh_at_g, const uint32_t *ug_at_h, auto hc) BS_INL {
             constexpr int h = decltype(hc)::value;
             const uint32_t zh = uint32_t(c * 4 + h);
+            uint32_t c12[16];
+            if constexpr (CSE) {
+                K6::pft_pair(uh_at_g, ug_at_h, c12);  // both outputs through shared subexpressions
+            } else {
+                uint32_t c1[8], c2[8];
+                K6::pft(uh_at_g, ug_at_h, c1);
+                K6::pft(ug_at_h, uh_at_g, c2);
+#pragma unroll
+                for (int w = 0; w < 8; w++) {
+                    c12[w] = c1[w];
+                    c12[8 + w] = c2[w];
+                }
+            }
             uint32_t c1[8], c2[8];
-            K6::pft(uh_at_g, ug_at_h, c1);  // C[h][z_G]
-            put<h>(a, c1, zg, t, prel, ragged);
-            K6::pft(ug_at_h, uh_at_g, c2);  // C[G][z_h]
-            put<G>(a, c2, zh, t, prel, ragged);
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+                c1[w] = c12[w];
+                c2[w] = c12[8 + w];
+            }
+            put<h>(a, c1, zg, t, prel, ragged);  // C[h][z_G]
+            put<G>(a, c2, zh, t, prel, ragged);  // C[G][z_h]
         };
         auto keep = [&](int ri, int p) BS_INL {
 #pragma unroll

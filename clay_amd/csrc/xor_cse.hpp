@@ -29,11 +29,13 @@ constexpr int cse_popc(uint32_t v) {
 }
 constexpr int cse_cost(int w) { return w <= 0 ? 0 : (w + 1) / 2; }
 
-template <int NR>
+// NIN input operands (8 bit-planes of one node, or 16 for a PFT pair)
+template <int NR, int NIN = 8>
 constexpr XorCse make_xor_cse(const uint32_t (&in)[NR]) {
+    static_assert(NIN + kCseMaxT <= 32 && NR <= 32, "operand masks are 32 bits");
     XorCse c{};
     for (int r = 0; r < NR; r++) c.row[r] = in[r];
-    int nops = 8;
+    int nops = NIN;
     while (c.nt < kCseMaxT) {
         int best = 0, bi = -1, bj = -1, bk = -1;
         for (int i = 0; i < nops; i++)
@@ -81,17 +83,17 @@ constexpr XorCse make_xor_cse(const uint32_t (&in)[NR]) {
 // acc[o] (^)= the CSE program F::C applied to the 8 input planes u, outputs o < NOUT
 // (ACC = false: the first fold into uninitialised accumulators).  Needs bitslice.hpp (sfor,
 // xor3, xor_sel) included first.
-template <class F, int NOUT, bool ACC>
-__device__ __forceinline__ void cse_fold(const uint32_t (&u)[8], uint32_t *acc) {
-    uint32_t ext[8 + kCseMaxT];
+template <class F, int NOUT, bool ACC, int NIN = 8>
+__device__ __forceinline__ void cse_fold(const uint32_t (&u)[NIN], uint32_t *acc) {
+    uint32_t ext[NIN + kCseMaxT];
 #pragma unroll
-    for (int w = 0; w < 8; w++) ext[w] = u[w];
+    for (int w = 0; w < NIN; w++) ext[w] = u[w];
     sfor<kCseMaxT>([&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
         if constexpr (k < F::C.nt) {
             constexpr int o0 = F::C.t[k][0], o1 = F::C.t[k][1], o2 = F::C.t[k][2];
-            if constexpr (o2 == 255) ext[8 + k] = ext[o0] ^ ext[o1];
-            else ext[8 + k] = xor3(ext[o0], ext[o1], ext[o2]);
+            if constexpr (o2 == 255) ext[NIN + k] = ext[o0] ^ ext[o1];
+            else ext[NIN + k] = xor3(ext[o0], ext[o1], ext[o2]);
         }
     });
     sfor<NOUT>([&](auto oc) __attribute__((always_inline)) {
