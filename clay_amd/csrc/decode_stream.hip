@@ -80,6 +80,9 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
         case 15: return launch_split<10, 3, 4>(a, stream, dev);
         case 16: return launch_split<10, 3, 8, 1>(a, stream, dev);   // solve only, no presolve
         case 17: return launch_split<10, 3, 16, 1>(a, stream, dev);  // solve only, no rounds
+        case 18: return launch_split<10, 3, 3, 1>(a, stream, dev);   // solve only: S DMA only
+        case 19: return launch_split<10, 3, 5, 1>(a, stream, dev);   // solve only: output stores only
+        case 20: return launch_split<10, 3, 1, 1>(a, stream, dev);   // solve only: DMA + stores
         default: break;
         }
     }
