@@ -368,12 +368,13 @@ struct BsRepairStream {
             for (int j = 0; j < BPL; j++) dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.roff[j] + L.k16[j]);
         } else {
             // partial tile (the last of the sub-chunk, vend = sc >= 16): a piece straddling vend
-            // is read from vend - 16 and rewritten by patch(), a piece wholly past it from b0
+            // is read from vend - 16 and rewritten by patch(); a piece wholly past it from vend - 16
+            // too (never used; b0 + 16 may lie past the row when the tile is under 16 bytes)
             const uint8_t *base = uniform_ptr(node);
 #pragma unroll
             for (int j = 0; j < BPL; j++) {
                 uint32_t pos = b0 + L.k16[j];
-                if (pos + 16u > vend) pos = pos >= vend ? b0 : vend - 16u;
+                if (pos + 16u > vend) pos = vend - 16u;
                 dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.roff[j] + pos);
             }
         }

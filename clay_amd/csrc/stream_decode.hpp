@@ -177,7 +177,7 @@ struct StreamDec {
             // of that part reads the slot's upper half), a piece wholly past vend from b0
             const uint8_t *base = uniform_ptr(node);
             uint32_t pos = t.b0 + L.pc16;
-            if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
+            if (pos + 16u > t.vend) pos = t.vend - 16u;  // past vend: unused; vend >= 16 (sc >= 512)
 #pragma unroll
             for (int j = 0; j < BPL; j++)
                 dma16(lds_buf + uint32_t(li * BPL + j) * 1024u, base, L.off[j] - L.pc16 + pos);

@@ -158,7 +158,7 @@ struct StreamEnc {
                     // after landing), a piece wholly past vend from b0 (never used)
                     const uint8_t *base = uniform_ptr(a.data[node] + uint64_t(g) * sc);
                     uint32_t pos = t.b0 + L.k16;
-                    if (pos + 16u > t.vend) pos = pos >= t.vend ? t.b0 : t.vend - 16u;
+                    if (pos + 16u > t.vend) pos = t.vend - 16u;  // past vend: unused; vend = sc >= 16
 #pragma unroll
                     for (int j = 0; j < BPL; j++) dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
                 }
