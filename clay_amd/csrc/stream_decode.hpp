@@ -476,30 +476,34 @@ struct StreamDec {
         }
         lds_barrier();  // every C of the tile in LDS
     }
-    // rounds3: the same corrections, one work item per (pair, dword): the pair's term
-    // A_(Y,X)[r] C(e_Y, z[Y:=X]) of one dword for every r, XORed into C_r(z) with LDS atomics.
+    // rounds3: the same corrections, one work item per (pair, 8 bytes): the pair's term
+    // A_(Y,X)[r] C(e_Y, z[Y:=X]) of 8 positions for every r, XORed into C_r(z) with 64-bit LDS
+    // atomics (ds_xor_b64).  Rounds of the 4-erasure 1 GiB decode: 0.087 ms (4-byte items 0.124,
+    // 16-byte items 0.097).
     // A round's latency is then its item count / 1024 instead of its layers' term count.
     __device__ static void rounds3(const DecArgs &a, uint8_t *scb0, const uint8_t *tl, uint32_t tid) {
         const uint32_t nround = a.nround;
         const uint16_t *pairs = reinterpret_cast<const uint16_t *>(tl + kDecPairs * 4);
         for (uint32_t rd = a.round1; rd < nround; rd++) {
             lds_barrier();  // C of the previous round visible
-            const uint32_t i0 = a.pstart[rd] * 32u, i1 = a.pstart[rd + 1] * 32u;
+            // items of 8 bytes: 16 per pair (one 128-byte row)
+            const uint32_t i0 = a.pstart[rd] * 16u, i1 = a.pstart[rd + 1] * 16u;
             for (uint32_t i = i0 + tid; i < i1; i += 1024u) {
-                const uint32_t pr = pairs[i >> 5], d4 = (i & 31u) * 4u;
+                const uint32_t pr = pairs[i >> 4], d8 = (i & 15u) * 8u;
                 const uint32_t z = pr & 255u, Y = (pr >> 8) & 3u, X = pr >> 10;
                 const uint32_t sh = 2u * (3u - Y), zy = (z >> sh) & 3u;
                 const uint32_t zs = z + ((X - zy) << sh);  // z[Y := X]
                 const int ry = a.rix[4 * Y + zy];           // the erased node of section Y (red in z)
-                const uint32_t cv = *reinterpret_cast<const uint32_t *>(scb0 + uint32_t(ry) * SBUF + zs * SW + d4);
-                const GfIdx ix = gf_idx(cv);
+                const uint2 cv = *reinterpret_cast<const uint2 *>(scb0 + uint32_t(ry) * SBUF + zs * SW + d8);
+                const GfIdx ix0 = gf_idx(cv.x), ix1 = gf_idx(cv.y);
                 const uint8_t *tb = tl + (16u + (Y * 4u + X) * 4u) * 32u;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     if (uint32_t(r) >= a.ne) break;
                     const GfTab t = tab_at(tb, r);
-                    __hip_atomic_fetch_xor(reinterpret_cast<uint32_t *>(scb0 + r * SBUF + z * SW + d4), gf_mul_idx(ix, t),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint64_t v = uint64_t(gf_mul_idx(ix0, t)) | (uint64_t(gf_mul_idx(ix1, t)) << 32);
+                    __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scb0 + r * SBUF + z * SW + d8), v, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
