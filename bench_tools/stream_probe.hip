@@ -85,6 +85,16 @@ int main(int argc, char **argv) {
     };
     for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
     (void)hipDeviceSynchronize();
+    if (argc > 2 && argv[2][0] == 'l') {  // steady state: loader-wave count
+        printf("sc %u back-to-back loader sweep\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b L4 full", run_b2b<4, 0>(a, 200));
+            rep("b2b L2 full", run_b2b<2, 0>(a, 200));
+            rep("b2b L1 full", run_b2b<1, 0>(a, 200));
+            rep("b2b L4 full, loaders prio 0", run_b2b<4, 8>(a, 200));
+        }
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'b') {  // steady state, back-to-back launches
         printf("sc %u back-to-back (200 launches after 50 untimed)\n", sc);
         for (int rr = 0; rr < 3; rr++) {

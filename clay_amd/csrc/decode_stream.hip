@@ -31,7 +31,7 @@ static hipError_t launch_one(const bs::DecArgs &a, hipStream_t stream, int dev) 
     return hipGetLastError();
 }
 
-template <int KD, int G, int SPROBE = 0, int SKIP = 0>
+template <int KD, int G, int SPROBE = 0, int SKIP = 0, int YPROBE = 0>
 static hipError_t launch_split(const bs::DecArgs &a, hipStream_t stream, int dev) {
     using Kn = bs::StreamDec<KD, G>;
     static std::mutex mu;
@@ -39,7 +39,7 @@ static hipError_t launch_split(const bs::DecArgs &a, hipStream_t stream, int dev
     {
         std::lock_guard<std::mutex> lk(mu);
         if (!done.count(dev)) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_syn<KD, G>),
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_syn<KD, G, YPROBE>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
             if (e == hipSuccess)
                 e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_solve<KD, G, SPROBE>),
@@ -49,7 +49,7 @@ static hipError_t launch_split(const bs::DecArgs &a, hipStream_t stream, int dev
         }
     }
     if (!(SKIP & 1)) {
-        bs::k_stream_syn<KD, G><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        bs::k_stream_syn<KD, G, YPROBE><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -83,6 +83,8 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
         case 18: return launch_split<10, 3, 3, 1>(a, stream, dev);   // solve only: S DMA only
         case 19: return launch_split<10, 3, 5, 1>(a, stream, dev);   // solve only: output stores only
         case 20: return launch_split<10, 3, 1, 1>(a, stream, dev);   // solve only: DMA + stores
+        case 21: return launch_split<10, 3, 0, 2, 2>(a, stream, dev);  // syn only, no phase-A math
+        case 22: return launch_split<10, 3, 0, 2, 4>(a, stream, dev);  // syn only, no DMA
         default: break;
         }
     }
