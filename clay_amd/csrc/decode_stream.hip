@@ -85,6 +85,8 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
         case 20: return launch_split<10, 3, 1, 1>(a, stream, dev);   // solve only: DMA + stores
         case 21: return launch_split<10, 3, 0, 2, 2>(a, stream, dev);  // syn only, no phase-A math
         case 22: return launch_split<10, 3, 0, 2, 4>(a, stream, dev);  // syn only, no DMA
+        case 23: return launch_split<10, 3, 32, 1>(a, stream, dev);    // solve only, nt output stores
+        case 24: return launch_split<10, 3, 37, 1>(a, stream, dev);    // solve only, nt stores only
         default: break;
         }
     }

@@ -724,7 +724,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_syn(DecArg
 constexpr int kSolveLds = 4 * 256 * 128 + kDecTabWords * 4;  // S/C tile (128 positions) + tables, order, pairs
 
 // PROBE (CLAY_DECODE_PROBE, probe library only): bit 1 = no presolve / rounds, 2 = no HBM
-// stores, 4 = no S DMA, 8 = no presolve, 16 = no rounds.  grid = 8 * ns (one 1024-thread workgroup per CU); XCD x owns 128-byte
+// stores, 4 = no S DMA, 8 = no presolve, 16 = no rounds, 32 = non-temporal output stores.  grid = 8 * ns (one 1024-thread workgroup per CU); XCD x owns 128-byte
 // tiles [x * per, (x + 1) * per) (a.region = per * 128), its ns workgroups take them round robin.
 template <int KD, int G, int PROBE = 0>
 __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
@@ -803,7 +803,15 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
 #pragma unroll
                 for (uint32_t zz = 0; zz < 2; zz++) {
                     uint8_t *o = dst + uint64_t((threadIdx.x >> 3) + 128u * zz) * sc + b0 + q16;
-                    if (full) *reinterpret_cast<uint4 *>(o) = cv[r][zz];
+                    if (full) {
+                        if constexpr ((PROBE & 32) != 0) {  // probe: non-temporal output stores
+                            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                            const v4u v = {cv[r][zz].x, cv[r][zz].y, cv[r][zz].z, cv[r][zz].w};
+                            __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(o));
+                        } else {
+                            *reinterpret_cast<uint4 *>(o) = cv[r][zz];
+                        }
+                    }
                     else if (half) *reinterpret_cast<uint2 *>(o) = make_uint2(cv[r][zz].x, cv[r][zz].y);
                 }
             }
