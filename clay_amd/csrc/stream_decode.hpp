@@ -189,8 +189,7 @@ struct StreamDec {
     // section Y's alive nodes are loads qbase + sec_off[Y] .. of the ring (buffer = load % ring).
     template <int PROBE>
     __device__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
-                                   uint32_t (&S)[32]) {
-        const uint32_t R = a.ring;
+                                   uint32_t (&S)[32], uint32_t R) {  // R: ring depth (node buffers)
         sfor<4>([&](auto yc) BS_INL {
             constexpr int Y = decltype(yc)::value;
             lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
@@ -606,7 +605,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
         for (int w = 0; w < 32; w++) S[w] = 0;
 
         // ---------------- phase A: one step per section ----------------
-        Kn::template phase_a<PROBE>(a, smem, 0u, c0, poff0, xeG, S);
+        Kn::template phase_a<PROBE>(a, smem, 0u, c0, poff0, xeG, S, R);
 
         // ---------------- S_known -> LDS (S/C region, [j][z][p]) ----------------
         lds_barrier();  // B0: every wave is done with the ring buffers of tile k
@@ -639,8 +638,9 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
 // Split decode: the same two phases in two launches, so that phase B (latency-bound rounds behind
 // workgroup barriers, no memory traffic of its own) no longer stalls the streaming of phase A.
 //  k_stream_syn   phase A of every tile with the ring streaming continuously across tiles (global
-//                 load index -> buffer), S of tile b0 written to ws + b0 * 1024 (64 KiB per
-//                 64-byte tile, [j][z][64 B] as the fused kernel's S/C region)
+//                 load index -> buffer), then the presolve S' = H_K^-1 S; S' of tile b0 written to
+//                 ws + b0 * 1024 (64 KiB per 64-byte tile, [r][z][64 B] as the fused kernel's S/C
+//                 region)
 //  k_stream_solve phase B: two workgroups per CU (64 KiB S/C tile + 3 KiB tables each), one tile
 //                 at a time: LDS-DMA of the S tile, the rounds (StreamDec::rounds), C to HBM; the
 //                 other workgroup of the CU overlaps its rounds with this one's DMA.
@@ -656,7 +656,8 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_syn(DecArg
     const typename Kn::Map tm(sc, a.region, ns, xcd, wslot);
     const uint32_t ntile = tm.n;
     if (ntile == 0) return;  // uniform per workgroup
-    const uint32_t R = a.ring, NT = a.nt;
+    // ring of a.ring - 1 node buffers; the last buffer holds the presolve tables (H_K^-1 rows)
+    const uint32_t R = a.ring - 1u, NT = a.nt;
     constexpr uint32_t BUF = uint32_t(Kn::BUF);
 
     if (wave >= Kn::CWAVES) {
@@ -666,6 +667,9 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_syn(DecArg
         typename Kn::Loader L;
         Kn::loader_init(L, sc, li, lane);
         const uint32_t lds0 = lds_addr_of(smem);
+        if (li < 3)  // tables, before any ring load: the first step's counted wait covers them
+            dma16(lds0 + R * BUF + uint32_t(li) * 1024u, uniform_ptr(reinterpret_cast<const uint8_t *>(a.tabs)),
+                  uint32_t(li) * 1024u + uint32_t(lane) * 16u);
         const uint32_t nloads = ntile * NT;
         uint32_t issued = 0;
         auto issue_upto = [&](uint32_t lim) {
@@ -702,22 +706,44 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_syn(DecArg
         uint32_t S[32];
 #pragma unroll
         for (int w = 0; w < 32; w++) S[w] = 0;
-        Kn::template phase_a<PROBE>(a, smem, k * NT, c0, poff0, xeG, S);
-        // S -> the workspace tile ([j][z][p] x 8 B)
-        const uint32_t c = opq(c0);
-        const uint32_t z0 = Kn::layer0(c);
-        uint8_t *wtile = a.ws + uint64_t(t.b0) * 1024u + 8u * p;
-        sfor<4>([&](auto jc) BS_INL {
-            constexpr int j = decltype(jc)::value;
+        Kn::template phase_a<PROBE>(a, smem, k * NT, c0, poff0, xeG, S, R);
+        // S back to bytes, then the presolve S' = H_K^-1 S (run-time v_perm tables from LDS; the
+        // kernel is memory-bound, so this VALU work hides under the streaming), S' -> the
+        // workspace tile ([r][z][p] x 8 B)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
             uint32_t v[8];
 #pragma unroll
             for (int w = 0; w < 8; w++) v[w] = S[j * 8 + w];
             transpose8(v);
 #pragma unroll
-            for (int g = 0; g < 4; g++)
-                *reinterpret_cast<uint2 *>(wtile + uint32_t(j) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) =
-                    make_uint2(v[2 * g], v[2 * g + 1]);
-        });
+            for (int w = 0; w < 8; w++) S[j * 8 + w] = v[w];
+        }
+        const uint32_t c = opq(c0);
+        const uint32_t z0 = Kn::layer0(c);
+        uint8_t *wtile = a.ws + uint64_t(t.b0) * 1024u + 8u * p;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            uint32_t U[4][2] = {};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                // tables re-read per (g, j) through an opaque address: 4 live at a time instead of
+                // all 16 hoisted into registers
+                const uint8_t *tl = smem + R * BUF + opq(0u);
+                const GfIdx i0 = gf_idx(S[j * 8 + 2 * g]), i1 = gf_idx(S[j * 8 + 2 * g + 1]);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const GfTab tb = Kn::tab_at(tl, r * 4 + j);
+                    U[r][0] ^= gf_mul_idx(i0, tb);
+                    U[r][1] ^= gf_mul_idx(i1, tb);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                *reinterpret_cast<uint2 *>(wtile + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) =
+                    make_uint2(U[r][0], U[r][1]);
+        }
     }
 }
 
@@ -774,7 +800,7 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
         else wait_vm_rt(PROBE & 2 ? 0 : int(nstores));  // S of tile k (tile k-1's stores may stay in flight)
         lds_barrier();  // S (and, first time, the tables) landed
         if constexpr (!(PROBE & 1)) {
-            if constexpr (!(PROBE & 8)) Kn::presolve(smem, tl, c0, p);
+            // S' arrives presolved (k_stream_syn): only the rounds
             if constexpr (!(PROBE & 16)) Kn::rounds3(a, smem, tl, threadIdx.x);  // ends with a barrier
             else lds_barrier();
         } else {
