@@ -92,6 +92,9 @@ def launch(args, argv) -> int:
     once instead of leaving them blocked in a barrier -- the launcher then exits with that
     rank's code.  The parent never touches HIP."""
     port = _free_port()
+    # build the CPU checker once here (CPU only, no HIP) so the ranks never race on make
+    from oracle import oracle
+    oracle.build()
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ)

@@ -109,16 +109,16 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
-_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3}
+_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-fused": 4}
 
 
 def set_exec_mode(mode: str) -> str:
     """Process-wide plan executor for decode / repair / staged encode: 'auto' (tile-fused
     where the U slots fit in LDS, else grouped; the split streaming decode for >= 3 erasures of
     q = 4, t = 4 codes; the bit-sliced repair kernels for q = m repairs from all n - 1 nodes),
-    'grouped' (one launch per level), 'tile', or 'stream' (the split streaming decode for every
-    eligible q = 4, t = 4 decode -- CLAY_DECODE_SPLIT=0: the fused single-launch kernel -- else
-    as auto).  Every mode produces the reference's bytes.  Returns the previous mode."""
+    'grouped' (one launch per level), 'tile', 'stream' (the split streaming decode for every
+    eligible q = 4, t = 4 decode, else as auto) or 'stream-fused' (as 'stream' on the fused
+    single-launch decode kernel).  Every mode produces the reference's bytes.  Returns the previous mode."""
     if mode not in _EXEC_MODES:
         raise ValueError(f"unknown exec mode {mode!r}")
     prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])

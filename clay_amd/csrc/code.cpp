@@ -1,9 +1,11 @@
 // code.cpp -- parameters and validation with the reference's error precedence.
 #include "code.hpp"
+#include "tuning.hpp"
 
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 
 namespace clay {
 
@@ -253,5 +255,37 @@ Error validate_repair(const clay_code_t &c, size_t lost, const size_t *ids, cons
     }
     return Error{};
 }
+
+// ---- tuning knobs: read once, at load time (tuning.hpp) ----
+static Tuning read_tuning() {
+    Tuning t;
+    auto ival = [](const char *name, long long def) -> long long {
+        const char *e = getenv(name);
+        return e && *e ? atoll(e) : def;
+    };
+    t.plan_inline = ival("CLAY_PLAN_INLINE", 1) == 0 ? 0 : 1;
+    t.plan_dup = int(ival("CLAY_PLAN_DUP", -1));
+    t.plan_fold_cost = int(ival("CLAY_PLAN_FOLD_COST", -1));
+    t.plan_defer_out = int(ival("CLAY_PLAN_DEFER_OUT", -1));
+    t.plan_merge_slack = int(ival("CLAY_PLAN_MERGE_SLACK", -1));
+    t.plan_debug = getenv("CLAY_PLAN_DEBUG") != nullptr;
+    const long long w = ival("CLAY_TEXEC_WAVES", 0);
+    t.texec_waves = w == 4 || w == 8 || w == 16 ? int(w) : 0;
+    t.texec_lds = size_t(ival("CLAY_TEXEC_LDS_KB", 80)) * 1024;
+    t.texec_big = ival("CLAY_TEXEC_BIG", 0) != 0;
+    t.gexec_pipe = ival("CLAY_GEXEC_PIPE", 1) != 0;
+    t.gexec_order = uint32_t(ival("CLAY_GEXEC_ORDER", 2));
+    const long long tpw = ival("CLAY_GEXEC_TPW", 0);
+    t.gexec_tpw = tpw >= 1 && tpw <= 64 ? int(tpw) : 0;
+    t.gexec_small = uint64_t(ival("CLAY_GEXEC_SMALL", 2048));
+    t.gexec_big = uint64_t(ival("CLAY_GEXEC_BIG", 32768));
+    t.host_piece = size_t(ival("CLAY_HOST_PIECE_MB", 256)) << 20;
+    t.host_streams = int(ival("CLAY_HOST_STREAMS", 2));
+    t.decode_probe = int(ival("CLAY_DECODE_PROBE", 0));
+    return t;
+}
+// namespace-scope: initialised when the library is loaded, before any ABI call
+static const Tuning g_tuning = read_tuning();
+const Tuning &tuning() { return g_tuning; }
 
 }  // namespace clay

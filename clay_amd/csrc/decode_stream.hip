@@ -10,6 +10,7 @@
 #include <utility>
 
 #include "stream_decode.hpp"
+#include "tuning.hpp"
 
 namespace clay {
 
@@ -66,10 +67,7 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
 #ifdef CLAY_DECODE_PROBES
     // CLAY_DECODE_PROBE: skip parts of the kernel (measurement only: the probe library
     // libclay_amd_probe.so, `make probe`; the product library has no probe instantiations)
-    static const int probe = [] {
-        const char *e = getenv("CLAY_DECODE_PROBE");
-        return e ? atoi(e) : 0;
-    }();
+    const int probe = tuning().decode_probe;
     if (kd == 10 && probe && a.ws) {
         switch (probe) {  // split decode: 11 solve no work, 12 solve no stores, 13 syn only, 14 solve only,
                           // 15 solve no S DMA

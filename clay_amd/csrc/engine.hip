@@ -33,9 +33,11 @@
 #include "bitslice.hpp"
 #include "bitslice6.hpp"
 #include "stream_encode.hpp"
+#include "repair_args.hpp"  // bit-sliced repair kernel: repair_kernel.hpp, instantiated in repair_stream.hip
 #include "decode_args.hpp"  // streaming-decode kernel: stream_decode.hpp, instantiated in decode_stream.hip
 #include "kernels.hpp"
 #include "plan.hpp"
+#include "tuning.hpp"
 
 namespace clay {
 
@@ -898,11 +900,7 @@ static Error upload_vec(const std::vector<T> &v, const T **out) {
 // Waves per workgroup of the tile-fused executor: enough for the widest level's groups
 // (4 / 8 / 16), or CLAY_TEXEC_WAVES.
 static uint32_t texec_waves(const Plan &pl) {
-    static const int forced = [] {
-        const char *e = getenv("CLAY_TEXEC_WAVES");
-        const int v = e ? atoi(e) : 0;
-        return v == 4 || v == 8 || v == 16 ? v : 0;
-    }();
+    const int forced = tuning().texec_waves;
     if (forced) return uint32_t(forced);
     uint32_t mx = 0;
     for (size_t L = 0; L + 1 < pl.gstage_begin.size(); L++)
@@ -1049,10 +1047,7 @@ static void launch_gexec1(int mode, dim3 grid, dim3 block, hipStream_t stream, c
                           uint32_t tpw) {
     // software-pipelined source loads (default; CLAY_GEXEC_PIPE=0 disables): repair (9,3,11)
     // 0.330 -> 0.323 ms, decode 4 erasures 0.863 -> 0.855 ms (profiles/r02/gexec_pipe.txt)
-    static const bool pipe = [] {
-        const char *e = getenv("CLAY_GEXEC_PIPE");
-        return !(e && atoi(e) == 0);
-    }();
+    const bool pipe = tuning().gexec_pipe;
     auto k = mode == kBatchTable ? k_gexec<VW, MAXD, kBatchTable>
            : mode == kBatchAffine ? k_gexec<VW, MAXD, kBatchAffine>
            : pipe ? k_gexec<VW, MAXD, kBatchNone, true> : k_gexec<VW, MAXD, kBatchNone>;
@@ -1066,10 +1061,7 @@ static void launch_gexec(uint32_t maxd, dim3 grid, hipStream_t stream, const Exe
                          uint8_t *const *ptab = nullptr, const ExecStride *stride = nullptr, uint32_t nstripes = 1,
                          uint32_t lps = kExecBlock, uint32_t tpw = 1) {
     dim3 block(kExecBlock);
-    static const uint32_t order = [] {
-        const char *e = getenv("CLAY_GEXEC_ORDER");
-        return e ? uint32_t(atoi(e)) : 2u;
-    }();
+    const uint32_t order = tuning().gexec_order;
     static const ExecStride zero{};
     const ExecStride &S = stride ? *stride : zero;
     const uint32_t nb = n * tiles, bx = (nb + 7) / 8;
@@ -1089,15 +1081,9 @@ static int align_of(uintptr_t p) {
 }
 
 // Executor selection (clay_set_exec_mode): process-wide, read without locks.
-enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3 };  // see clay_set_exec_mode
+enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3, kExecStreamFused = 4 };  // see clay_set_exec_mode
 static std::atomic<int> g_exec_mode{kExecAuto};
-static size_t tex_lds_budget() {
-    static const size_t b = [] {
-        const char *e = getenv("CLAY_TEXEC_LDS_KB");
-        return size_t(e ? atoi(e) : 80) * 1024;
-    }();
-    return b;
-}
+static size_t tex_lds_budget() { return tuning().texec_lds; }
 // Lane width of the tile-fused executor for a plan (0 = not eligible): the widest of
 // 16 / 8 / 4 bytes whose tile of U slots (nu x 64 x VW) fits the LDS budget (default
 // 80 KiB: two workgroups per CU); failing that, 4-byte lanes with up to 160 KiB (one
@@ -1107,10 +1093,7 @@ static int texec_vw(const Plan &pl, uint32_t nu, uint32_t maxd) {
     if (stages == 0 || stages > size_t(kTexMaxStages) || maxd > 8 || nu == UINT32_MAX) return 0;
     for (int vw = 16; vw >= 4; vw >>= 1)
         if (uint64_t(nu) * 64 * vw + kTexTabBytes <= tex_lds_budget()) return vw;
-    static const bool big = [] {
-        const char *e = getenv("CLAY_TEXEC_BIG");
-        return e && atoi(e) != 0;
-    }();
+    const bool big = tuning().texec_big;
     if (big && uint64_t(nu) * 64 * 4 + kTexTabBytes <= kTexLdsMax) return 4;
     return 0;
 }
@@ -1157,14 +1140,13 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     // 0.038 ms.  On the big plans it measured slower than the grouped executor ((9,3,11)
     // repair 0.53 vs 0.43 ms, (10,4,13) 1-erasure decode 0.72 vs 0.41 ms),
     // so "tile" mode runs it wherever eligible but auto does not.
-    const bool tex_ok = xm == kExecTile || ((xm == kExecAuto || xm == kExecStream) && pl.groups.size() <= kTexAutoGroups &&
+    const bool tex_ok = xm == kExecTile || (xm != kExecGrouped && pl.groups.size() <= kTexAutoGroups &&
                                              pl.gstage_begin.size() > 2);  // one level: nothing to fuse
     if (tex_ok && sc > 0 && sc / (64 * 4) < 0x7fffffffu) {
         uint32_t maxd = 1;
         for (uint32_t m : pl.gstage_maxd) maxd = std::max(maxd, m);
         const int vw = texec_vw(pl, g.nu, maxd);
-        static const bool dbg = getenv("CLAY_PLAN_DEBUG") != nullptr;
-        if (dbg) fprintf(stderr, "run_plan: %zu levels, %u LDS U slots, maxd %u -> tile executor vw %d\n",
+        if (tuning().plan_debug) fprintf(stderr, "run_plan: %zu levels, %u LDS U slots, maxd %u -> tile executor vw %d\n",
                          pl.gstage_begin.size() - 1, g.nu, maxd, vw);
         if (vw) {
             const uint32_t nst = uint32_t(pl.gstage_begin.size() - 1), ub = 2 * pl.tn;
@@ -1193,19 +1175,8 @@ static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipS
     // mid-size levels of wide groups cost 2x ((10,4,13) repair, 64 groups: 0.21 -> 0.40 ms),
     // hence the low threshold (profiles/r02/gexec_block_shape.txt).  CLAY_GEXEC_TPW fixes
     // the tiles per block for every level.
-    static const int tpw_env = [] {
-        const char *e = getenv("CLAY_GEXEC_TPW");
-        const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= 64 ? v : 0;
-    }();
-    static const uint64_t small_wg = [] {
-        const char *e = getenv("CLAY_GEXEC_SMALL");
-        return uint64_t(e ? atoll(e) : 2048);
-    }();
-    static const uint64_t big_wg = [] {
-        const char *e = getenv("CLAY_GEXEC_BIG");
-        return uint64_t(e ? atoll(e) : 32768);
-    }();
+    const int tpw_env = tuning().gexec_tpw;
+    const uint64_t small_wg = tuning().gexec_small, big_wg = tuning().gexec_big;
     const uint32_t tiles16 = uint32_t((sc / 16 + 1 + kExecBlock - 1) / kExecBlock);
     const uint32_t tiles4 = uint32_t((sc / 4 + 1 + kExecBlock - 1) / kExecBlock);
     for (size_t s = 0; s + 1 < pl.gstage_begin.size(); s++) {
@@ -1777,7 +1748,7 @@ hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t
 template <int KD>
 static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &prop, const uint8_t *const *cin,
                                   uint8_t *const *cout, const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream,
-                                  bool *done) {
+                                  bool split, bool *done) {
     *done = false;
     const clay_code_t &c = cs.code;
     using S = bs::Shape<KD, 4>;
@@ -1929,9 +1900,7 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         a.tabs = it->second;
     }
     // split decode (k_stream_syn + k_stream_solve, S through a pooled workspace of 64 KiB per
-    // 64-byte tile) unless CLAY_DECODE_SPLIT=0 selects the fused single-launch kernel
-    const char *sv = getenv("CLAY_DECODE_SPLIT");  // read per call: tests A/B both kernels
-    const bool split = !(sv && sv[0] == '0');
+    // 64-byte tile) unless exec mode "stream-fused" selects the fused single-launch kernel
     LeaseGuard ws(ds, stream);
     if (split) {
         Error le = lease_acquire(ds, (sc + 63) / 64 * 65536, stream, &ws.l);
@@ -1997,7 +1966,7 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     const int xmode = g_exec_mode.load(std::memory_order_relaxed);
     size_t n_erased = 0;
     for (size_t in = 0; in < tn; in++) n_erased += erased[in] && !(in >= c.k && in < c.k + c.nu) ? 1 : 0;
-    if ((xmode == kExecStream || (xmode == kExecAuto && n_erased >= 3)) && tn == 16) {
+    if ((xmode == kExecStream || xmode == kExecStreamFused || (xmode == kExecAuto && n_erased >= 3)) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};
         for (size_t i = 0; i < c.n; i++) {
@@ -2008,8 +1977,10 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         bool done = false;
         const DevProps &prop = dev_props(dev);
         const size_t sc = chunk / c.sub_chunk_no;
-        if (c.k == 10) e = launch_stream_decode<10>(cs, *ds, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
-        else if (c.k == 9) e = launch_stream_decode<9>(cs, *ds, prop, cin, cout, erased, sc, static_cast<hipStream_t>(stream), &done);
+        const bool split = xmode != kExecStreamFused;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (c.k == 10) e = launch_stream_decode<10>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
+        else if (c.k == 9) e = launch_stream_decode<9>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
         if (e || done) return e;
     }
     return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
@@ -2017,15 +1988,6 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
 
 // repair_stream.hip: bit-sliced repair kernel (repair_kernel.hpp); 1 launched, 0 no
 // instantiation for (k, m), < 0 HIP error
-namespace bs {
-struct RepArgs {
-    const uint8_t *h[16];
-    uint8_t *out;
-    uint64_t sc;
-    uint32_t x0, full, ntiles, per_xcd;
-    uint64_t b_start;
-};
-}  // namespace bs
 int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream, int dev, int cus,
                             int stream_mode, int *launches);
 
@@ -2054,7 +2016,7 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
     // helper (no aloof nodes); auto and "stream" exec modes ((9,3,11) 256 MiB chunks: 0.345-0.357
     // vs 0.39-0.41 ms grouped on the same boxes, profiles/r03/)
     const int xm = g_exec_mode.load(std::memory_order_relaxed);
-    if ((xm == kExecAuto || xm == kExecStream) && c.q == c.m && tn <= 16 && nh + 1 == c.n) {
+    if ((xm == kExecAuto || xm == kExecStream || xm == kExecStreamFused) && c.q == c.m && tn <= 16 && nh + 1 == c.n) {
         bs::RepArgs ra{};
         const size_t lost_int = internal_of(c, lost);
         bool ok = true;
@@ -2072,7 +2034,7 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
             // always in exec mode "stream"
             int nl = 0;
             const int r = launch_bs_repair_kernel(int(c.k), int(c.m), int(lost_int / c.q), ra, static_cast<hipStream_t>(stream),
-                                                  dev, dev_props(dev).cus, xm == kExecStream ? 2 : 1, &nl);
+                                                  dev, dev_props(dev).cus, xm == kExecAuto ? 1 : 2, &nl);
             if (r < 0) return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: %s", hipGetErrorString(hipError_t(-r)));
             if (r > 0) {
                 t_last_launches += nl;
@@ -2164,14 +2126,8 @@ static Error host_pipeline(int device, size_t sc, const std::vector<HostIn> &ins
     if (sc == 0 || all_rows == 0) return Error{};
     // default: 256 MiB of input per piece over 2 streams (scripts/sweep_host_api.sh), whole
     // 256-byte tiles; CLAY_HOST_PIECE_MB / CLAY_HOST_STREAMS override the defaults
-    static const size_t def_piece = [] {
-        const char *e = getenv("CLAY_HOST_PIECE_MB");
-        return (e ? size_t(atoi(e)) : size_t(256)) << 20;
-    }();
-    static const int def_streams = [] {
-        const char *e = getenv("CLAY_HOST_STREAMS");
-        return e ? atoi(e) : 2;
-    }();
+    const size_t def_piece = tuning().host_piece;
+    const int def_streams = tuning().host_streams;
     if (n_streams <= 0) n_streams = def_streams;
     size_t w = piece_bytes ? piece_bytes : def_piece / std::max<size_t>(1, in_rows);
     w = w >= 256 ? w / 256 * 256 : (w + 7) / 8 * 8;
@@ -2290,7 +2246,8 @@ int clay_set_encode_path(int mode) {
     return prev;
 }
 int clay_set_exec_mode(int mode) {
-    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream) return -1;
+    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream && mode != kExecStreamFused)
+        return -1;
     return g_exec_mode.exchange(mode);
 }
 const char *clay_last_encode_path(void) { return t_last_path.c_str(); }

@@ -8,6 +8,7 @@
 #include <string>
 
 #include "gf256.hpp"
+#include "tuning.hpp"
 
 namespace clay {
 
@@ -74,12 +75,7 @@ void PlanBuilder::emit(uint64_t dst, const std::vector<std::pair<uint64_t, uint8
 // linear map is unchanged; the U round trip through HBM disappears and the
 // consumer group reads the inputs directly.  CLAY_PLAN_INLINE=0 disables.
 void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
-    static int enabled = -1;
-    if (enabled < 0) {
-        const char *e = getenv("CLAY_PLAN_INLINE");
-        enabled = (e && e[0] == '0') ? 0 : 1;
-    }
-    if (!enabled) return;
+    if (!tuning().plan_inline) return;
     const size_t n = ops.size();
     std::unordered_map<uint64_t, int> written;
     for (const auto &o : ops) written[o.dst] = 1;
@@ -96,10 +92,7 @@ void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
             if (t.ver >= 0 && std::find(rl[t.ver].begin(), rl[t.ver].end(), rslot(o.dst)) == rl[t.ver].end())
                 rl[t.ver].push_back(rslot(o.dst));
     const GF &gf = GF::get();
-    static const int dup_env = [] {
-        const char *e = getenv("CLAY_PLAN_DUP");
-        return e ? atoi(e) : -1;
-    }();
+    const int dup_env = tuning().plan_dup;
     const size_t dup_max = size_t(dup_env >= 0 ? dup_env : dup_cost);
     // all sources of op p are final versions (nothing rewrites them afterwards)
     auto final_srcs = [&](size_t p) {
@@ -146,10 +139,7 @@ void PlanBuilder::inline_inputs(const std::vector<uint64_t> &outputs) {
         }
         if (is_out[i]) continue;
         const size_t ns = ops[i].src.size(), r = rl[i].size();
-        static const int cost_env = [] {
-            const char *e = getenv("CLAY_PLAN_FOLD_COST");
-            return e ? atoi(e) : -1;
-        }();
+        const int cost_env = tuning().plan_fold_cost;
         const int cost_fold = cost_env >= 0 ? cost_env : fold_cost;
         // sources: never-written inputs (any reader count), or final versions of
         // computed regions when at most 2 ops read this one (folding then never
@@ -202,10 +192,7 @@ std::unique_ptr<Plan> PlanBuilder::finalize(const std::vector<uint64_t> &outputs
     // write a final output nothing reads, over final source versions, move from their
     // earliest level to the last one -- the tail levels fill with independent work
     // instead of idling at level boundaries.
-    static const int defer_env = [] {
-        const char *e = getenv("CLAY_PLAN_DEFER_OUT");
-        return e ? atoi(e) : -1;
-    }();
+    const int defer_env = tuning().plan_defer_out;
     if ((defer_env >= 0 ? defer_env != 0 : defer_outputs) && max_level > 2) {
         std::vector<int> nread(n, 0);
         for (size_t i = 0; i < n; i++)
@@ -310,10 +297,7 @@ void Plan::group_ops() {
         // union adds at most merge_slack sources to the larger set, so e.g. repair's three
         // folded outputs of one layer (15 shared helper reads + one own companion each)
         // share one source pass; the merged coefficient rows hold 0 for absent sources.
-        static const int slack_env = [] {
-            const char *e = getenv("CLAY_PLAN_MERGE_SLACK");
-            return e ? atoi(e) : -1;
-        }();
+        const int slack_env = tuning().plan_merge_slack;
         const size_t slack = size_t(slack_env >= 0 ? slack_env : merge_slack);
         if (slack > 0 && gs.size() > 1) {
             std::vector<uint8_t> gone(gs.size(), 0);
@@ -353,8 +337,7 @@ void Plan::group_ops() {
                 if (!gone[a]) kept.push_back(std::move(gs[a]));
             gs = std::move(kept);
         }
-        static const bool dbg = getenv("CLAY_PLAN_DEBUG") != nullptr;
-        if (dbg) {
+        if (tuning().plan_debug) {
             size_t nsrc = 0, ndst = 0;
             std::map<size_t, size_t> hist;
             for (auto &g : gs) {

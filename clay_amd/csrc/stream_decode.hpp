@@ -641,9 +641,10 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_decode(Dec
 //                 load index -> buffer), then the presolve S' = H_K^-1 S; S' of tile b0 written to
 //                 ws + b0 * 1024 (64 KiB per 64-byte tile, [r][z][64 B] as the fused kernel's S/C
 //                 region)
-//  k_stream_solve phase B: two workgroups per CU (64 KiB S/C tile + 3 KiB tables each), one tile
-//                 at a time: LDS-DMA of the S tile, the rounds (StreamDec::rounds), C to HBM; the
-//                 other workgroup of the CU overlaps its rounds with this one's DMA.
+//  k_stream_solve phase B: one 1024-thread workgroup per CU (a 128-byte tile: 4 x 256 x 128 B of
+//                 S' + 5 KiB of tables, ~133 KiB of LDS), one tile at a time: LDS-DMA of the S'
+//                 tile, the term-parallel rounds (LDS atomics), C to HBM in 128-byte row runs,
+//                 with the next tile's S' DMA issued before the output stores.
 // Extra HBM traffic: S written and read once (2 x 4 x 256 x sc bytes).
 // ---------------------------------------------------------------------------------------------
 template <int KD, int G, int PROBE = 0>
@@ -769,7 +770,6 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
     if (wave < kDecTabWords / 256)  // tables, layer order, correction pairs: once per workgroup
         dma16(lds0 + 4u * Kn::SBUF + uint32_t(wave) * 1024u, uniform_ptr(reinterpret_cast<const uint8_t *>(a.tabs)),
               uint32_t(wave) * 1024u + uint32_t(lane) * 16u);
-    const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
     // S of phase-A tiles b0 and b0 + 64 (ws + b * 1024, [j][z][64 B]) into buffer j of the
     // [j][z][128 B] region: LDS block (j, 8 rows) <- 8 x 2 pieces of 64 B; 32 blocks, 2 per wave
     const uint32_t zl = uint32_t(lane) >> 3, q = (uint32_t(lane) & 7u) * 16u;

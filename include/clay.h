@@ -264,9 +264,10 @@ int clay_set_encode_path(int mode);
  *    CU; auto when the sub-chunk gives every CU a tile, stream for any sub-chunk >= 16 bytes
  *    of (9,3,11) / (10,4,13); last path "bs-repair-stream"), else k_bs_repair ("bs-repair"))
  *   3 stream  -- every eligible decode of q = 4, t = 4 codes (any erasure count) on the split
- *                streaming decode ("stream-split"; with the environment variable
- *                CLAY_DECODE_SPLIT=0 the fused single-launch k_stream_decode, "stream");
- *                everything else as auto
+ *                streaming decode ("stream-split"); everything else as auto
+ *   4 stream-fused -- as stream, but on the fused single-launch k_stream_decode ("stream")
+ * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
+ * (planner and executor tuning) are read once when the library is loaded.
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
  * unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);

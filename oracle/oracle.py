@@ -54,14 +54,29 @@ class OracleError(Exception):
         super().__init__(f"{self.name}: {self.msg}")
 
 
+def _stale(src: str) -> bool:
+    return not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)
+
+
 def build() -> str:
-    """Compile liboracle.so (gcc) if missing or stale."""
+    """Compile liboracle.so (gcc) if missing or stale.  Safe from several processes at once
+    (bench ranks, pytest-xdist workers): the check and the make run under an exclusive lock
+    on oracle/.build.lock, so one process builds and the others find a fresh library; the
+    Makefile also writes the library under a temporary name and renames it into place, so a
+    process that loads it never sees a half-written file."""
     src = os.path.join(_HERE, "clay_oracle.c")
     if os.environ.get("CLAY_ORACLE_LIB"):
         return _LIB_PATH
-    if (not os.path.exists(_LIB_PATH)
-            or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
-        subprocess.check_call(["make", "-s", "-C", _HERE])
+    if not _stale(src):
+        return _LIB_PATH
+    import fcntl
+    with open(os.path.join(_HERE, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if _stale(src):
+                subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return _LIB_PATH
 
 

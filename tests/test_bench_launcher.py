@@ -80,3 +80,31 @@ def test_bench_rank_rejects_missing_device():
                        capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
     assert r.returncode == 2
     assert "only 0 GPU(s) visible" in r.stderr
+
+
+def test_bench_launcher_builds_stale_oracle_once(oracle_mod, tmp_path):
+    """With a stale liboracle.so (clay_oracle.c newer than it, as a fresh checkout can leave
+    it), a world-2 run builds the checker exactly once -- in the launcher parent, before any
+    rank starts -- instead of N ranks running make on, and loading, the same file at once."""
+    src = os.path.join(ROOT, "oracle", "clay_oracle.c")
+    so = os.path.join(ROOT, "oracle", "liboracle.so")
+    st = os.stat(so)
+    os.utime(src, (st.st_atime, st.st_mtime + 5))  # the source is now newer than the library
+    log = tmp_path / "make.log"
+    wrapper = tmp_path / "make"
+    wrapper.write_text(f"#!/bin/sh\necho \"$@\" >> {log}\nexec /usr/bin/make \"$@\"\n")
+    wrapper.chmod(0o755)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    env["PATH"] = f"{tmp_path}:{env.get('PATH', '')}"
+    stripe = 10 * 256 * 2 * 64
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-dry",
+                        "--stripe-bytes", str(stripe), "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert all(d["per_rank"]["verified"])
+    makes = log.read_text().splitlines() if log.exists() else []
+    assert len(makes) == 1, makes
+    assert os.path.getmtime(so) >= os.path.getmtime(src)

@@ -38,11 +38,10 @@ def _patterns(c, seed, n3, n4):
 
 
 @pytest.fixture(params=["split", "fused"])
-def auto_exec(request, monkeypatch):
-    """exec mode "stream": the split decode (k_stream_syn + k_stream_solve, default) or the fused
-    single-launch kernel (CLAY_DECODE_SPLIT=0); yields the path name last_exec_path() reports."""
-    monkeypatch.setenv("CLAY_DECODE_SPLIT", "1" if request.param == "split" else "0")
-    prev = clay_amd.set_exec_mode("stream")
+def auto_exec(request):
+    """exec mode "stream": the split decode (k_stream_syn + k_stream_solve), or "stream-fused":
+    the fused single-launch kernel; yields the path name last_exec_path() reports."""
+    prev = clay_amd.set_exec_mode("stream" if request.param == "split" else "stream-fused")
     yield "stream-split" if request.param == "split" else "stream"
     clay_amd.set_exec_mode(prev)
 
