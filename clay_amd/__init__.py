@@ -139,6 +139,15 @@ def release_workspace(device: int = 0) -> None:
         _raise(rc, err)
 
 
+def release_captured(device: int = 0) -> None:
+    """Reclaim the pointer-table arena and the pooled workspaces that calls inside stream
+    captures left to their graphs; call once those graphs are destroyed (clay.h)."""
+    err = ClayErrorStruct()
+    rc = _lib.lib().clay_release_captured(int(device), C.byref(err))
+    if rc:
+        _raise(rc, err)
+
+
 def workspace_bytes(device: int = 0) -> int:
     """Device memory held by the device's buffer pool."""
     return int(_lib.lib().clay_workspace_bytes(int(device)))

@@ -54,6 +54,7 @@ SIGNATURES = {
                                                  C.c_int, _vp, _err_p]),
     "clay_reserve_workspace": (C.c_int, [_code_p, _sz, C.c_int, _err_p]),
     "clay_release_workspace": (C.c_int, [C.c_int, _err_p]),
+    "clay_release_captured": (C.c_int, [C.c_int, _err_p]),
     "clay_chunk_to_ygroup": (C.c_int, [_code_p, _sz, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p, _err_p]),
     "clay_ygroup_to_chunk": (C.c_int, [_code_p, _sz, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p, _err_p]),
     "clay_encode_device_strided": (C.c_int, [_code_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,

@@ -908,11 +908,22 @@ static uint32_t texec_waves(const Plan &pl) {
     return mx <= 8 ? 4u : mx <= 16 ? 8u : 16u;
 }
 
-static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::DevGrouped *out) {
+// A plan or table first needed inside a stream capture cannot be uploaded there (hipMalloc +
+// a blocking copy would invalidate the capture): the call fails instead, and the caller runs one
+// call of that shape (erasure pattern, lost node) outside the capture first.
+static Error not_prepared(const char *what) {
+    return make_error(CLAY_ERR_DEVICE, 0, 0, 0,
+                      "%s not prepared before stream capture: run one call of this shape outside the capture "
+                      "first (clay_reserve_workspace prepares the encode plan)", what);
+}
+
+static Error upload_groups(CodeState &cs, const Plan &pl, int dev, CodeState::DevGrouped *out,
+                           hipStream_t st = nullptr) {
     std::lock_guard<std::mutex> lk(cs.mu);
     auto key = std::make_pair(&pl, dev);
     auto it = cs.gplan.find(key);
     if (it == cs.gplan.end()) {
+        if (st && capturing(st)) return not_prepared("plan");
         CodeState::DevGrouped g{};
         Error e = upload_vec(pl.groups, &g.groups);
         if (!e) e = upload_vec(pl.gsrcs, &g.srcs);
@@ -1132,7 +1143,7 @@ static Error launch_texec(uint32_t maxd, const ExecPtrs &ptrs, const CodeState::
 static Error run_plan(CodeState &cs, const Plan &pl, int dev, DevState &ds, hipStream_t stream,
                       ExecPtrs ptrs, size_t sc, size_t chunk_for_ws) {
     CodeState::DevGrouped g{};
-    Error e = upload_groups(cs, pl, dev, &g);
+    Error e = upload_groups(cs, pl, dev, &g, stream);
     if (e) return e;
     const int xm = g_exec_mode.load(std::memory_order_relaxed);
     // auto: the tile executor only for small plans (at most kTexAutoGroups groups), where
@@ -1515,7 +1526,7 @@ static Error encode_staged_batch(CodeState &cs, DevState &ds, int dev, const uin
     if (e) return e;
     const Plan &pl = *plp;
     CodeState::DevGrouped g{};
-    e = upload_groups(cs, pl, dev, &g);
+    e = upload_groups(cs, pl, dev, &g, stream);
     if (e) return e;
     const uint64_t sc = chunk / c.sub_chunk_no;
     const uint32_t lanes = uint32_t(sc / 16 + 1);  // 16-byte lanes incl. the byte tail
@@ -1892,6 +1903,7 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         auto key = std::make_pair(std::vector<uint32_t>(tabs), prop.dev);
         auto it = cs.dtabs.find(key);
         if (it == cs.dtabs.end()) {
+            if (capturing(stream)) return not_prepared("streaming-decode pattern table");
             const uint32_t *d = nullptr;
             Error ue = upload_vec(tabs, &d);
             if (ue) return ue;
@@ -2425,6 +2437,29 @@ int clay_release_workspace(int device, clay_error_t *err) {
         free_table(it->second);
         it = ds->tables.erase(it);
     }
+    return 0;
+}
+
+int clay_release_captured(int device, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    DevState *ds;
+    Error e = dev_state(device, &ds);
+    if (e) return report(e, err);
+    DeviceGuard g(device);
+    // the caller has destroyed its graphs; a replay launched before may still be running
+    if (hipDeviceSynchronize() != hipSuccess)
+        return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: device synchronize failed"), err);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    for (auto &t : ds->captured)
+        if (t->users > 0)
+            return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "a stream capture is using the pointer-table arena"), err);
+    ds->captured.clear();
+    ds->cap_used = 0;
+    for (auto &l : ds->pool)
+        if (l->pinned && !l->busy) {
+            l->pinned = false;
+            l->used = false;
+        }
     return 0;
 }
 

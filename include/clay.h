@@ -214,14 +214,29 @@ int clay_repair_device_full_chunks(const clay_code_t *code, size_t lost_node, co
 
 /* Pre-allocate an idle pooled workspace for chunk_size (any stream may take it) and
  * build + upload the code's encode plan, so that a later call allocates nothing --
- * e.g. before stream capture.  Decode/repair plans depend on the erasure pattern:
- * run one call per pattern before capturing it. */
+ * e.g. before stream capture.  The workspace is q x t x chunk_size bytes, which covers
+ * every call of that chunk size: the grouped executor's U workspace (q t chunk_size)
+ * and the split streaming decode's S' workspace (64 KiB per 64-byte tile of the
+ * sub-chunk, i.e. 1,024 x sc bytes for sc = chunk_size / alpha: 430 MB for a 1 GiB
+ * (10,4,13) stripe), each held per in-flight call.  Decode/repair plans and the
+ * streaming decode's pattern tables depend on the erasure pattern: run one call per
+ * pattern before capturing it (a capture that needs an unprepared one fails with
+ * CLAY_ERR_DEVICE rather than allocating). */
 int clay_reserve_workspace(const clay_code_t *code, size_t chunk_size, int device,
                            clay_error_t *err);
 
 /* Free the device's idle pooled buffers (waiting for their last users' events) and
  * its unpinned batch pointer tables.  Buffers in use or owned by captured graphs stay. */
 int clay_release_workspace(int device, clay_error_t *err);
+
+/* Reclaim what calls made inside stream captures left to their graphs: the pointer tables of
+ * captured batch calls (a 4 MiB per-device arena; a captured batch of n stripes takes
+ * n x 130 x 8 bytes, so about a dozen 300-stripe captures fill it, after which capturing
+ * such calls fails with CLAY_ERR_DEVICE) and the pooled workspaces pinned to graphs.
+ * Call it once every graph captured from this library's calls on `device` has been
+ * destroyed; it synchronises the device first (a replay may still run).  Fails while a
+ * capture that uses the arena is in progress.  No reference counterpart. */
+int clay_release_captured(int device, clay_error_t *err);
 
 /* Bytes of device memory held by the device's buffer pool (tests / monitoring). */
 size_t clay_workspace_bytes(int device);

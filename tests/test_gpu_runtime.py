@@ -366,3 +366,111 @@ def test_ygroup_layout_and_repair(oracle_mod, torch_cuda, cfg, sc):
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), ref[lost]), lost
         assert np.array_equal(back.cpu().numpy(), ref[h0])
+
+
+def test_capture_arena_reclaimed(oracle_mod, torch_cuda):
+    """Pointer tables of batch calls inside stream captures come from a fixed per-device
+    arena (no allocation while capturing).  Captures of a 300-stripe non-affine batch fill it
+    after about a dozen graphs; clay_release_captured, once those graphs are destroyed,
+    gives it back, and later captures replay bit-exact."""
+    torch = torch_cuda
+    k, m, d = 6, 3, 8
+    c, o = ClayCode(k, m, d), oracle_mod.OracleClay(k, m, d)
+    n, sc = 300, 32
+    chunk = c.sub_chunk_no * sc
+    refs = [_stripe(o, k, chunk, 2100 + s) for s in range(n)]
+    perm = np.random.default_rng(11).permutation(n)
+    slot = {s: j for j, s in enumerate(perm)}
+    data = torch.from_numpy(np.concatenate([refs[s][:k] for s in perm])).cuda()
+    par = torch.full((n * m, chunk), 0xFF, dtype=torch.uint8, device="cuda")
+    dl = [data[slot[s] * k + i] for s in range(n) for i in range(k)]
+    pl = [par[slot[s] * m + i] for s in range(n) for i in range(m)]
+    st = torch.cuda.Stream()
+    clay_amd.release_captured(0)
+    c.reserve_workspace(n * chunk)
+    c.encode_device_batch(dl, pl, n, chunk, 0, st.cuda_stream)  # plan upload outside capture
+    st.synchronize()
+
+    def capture():
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            c.encode_device_batch(dl, pl, n, chunk, 0, torch.cuda.current_stream().cuda_stream)
+        return g
+
+    graphs, failed = [], None
+    for _ in range(20):
+        try:
+            graphs.append(capture())
+        except clay_amd.DeviceError as ex:
+            failed = str(ex)
+            break
+    assert failed is not None and "arena" in failed, (len(graphs), failed)
+    assert 8 <= len(graphs) <= 14, len(graphs)
+    par.fill_(0xFF)
+    torch.cuda.synchronize()
+    graphs[-1].replay()
+    torch.cuda.synchronize()
+    got = par.cpu().numpy()
+    for s in range(n):
+        assert np.array_equal(got[slot[s] * m:(slot[s] + 1) * m], refs[s][k:]), ("before release", s)
+    del graphs
+    clay_amd.release_captured(0)
+    for rep in range(3):  # more captures than the arena held before: each one reclaimed
+        g = capture()
+        par.fill_(0xFF)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        got = par.cpu().numpy()
+        for s in range(n):
+            assert np.array_equal(got[slot[s] * m:(slot[s] + 1) * m], refs[s][k:]), (rep, s)
+        del g
+        clay_amd.release_captured(0)
+
+
+def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda):
+    """A 4-erasure (10,4,13) decode on the split streaming decode inside a stream capture: the
+    reserved workspace covers its S' lease and one eager call of the pattern prepared its
+    tables, so the capture allocates nothing (the pool does not grow) and replays bit-exact on
+    new data.  A pattern never run before fails inside the capture with a clear error instead
+    of invalidating it."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    sc = 1024
+    chunk = c.sub_chunk_no * sc
+    er = [0, 4, 8, 12]
+    st = torch.cuda.Stream()
+    clay_amd.release_captured(0)
+    clay_amd.release_workspace(0)
+    c.reserve_workspace(chunk)
+    reserved = clay_amd.workspace_bytes(0)
+    assert reserved >= (sc + 63) // 64 * 65536
+    full = torch.from_numpy(_stripe(o, 10, chunk, 77)).cuda()
+    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+    args = ([None if j in er else full[j] for j in range(14)], er, [outs[j] if j in er else None for j in range(14)])
+    c.decode_device(*args, chunk, 0, st.cuda_stream)  # prepares the pattern's tables
+    st.synchronize()
+    assert clay_amd.last_exec_path() == "stream-split"
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        c.decode_device(*args, chunk, 0, torch.cuda.current_stream().cuda_stream)
+    assert clay_amd.workspace_bytes(0) == reserved
+    for rep in range(2):
+        ref = _stripe(o, 10, chunk, 780 + rep)
+        full.copy_(torch.from_numpy(ref))
+        outs.fill_(0xA5)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for e in er:
+            assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (rep, e)
+    er2 = [1, 5, 9, 13]
+    g2 = torch.cuda.CUDAGraph()
+    with pytest.raises(clay_amd.DeviceError, match="not prepared"):
+        with torch.cuda.graph(g2, stream=st):
+            c.decode_device([None if j in er2 else full[j] for j in range(14)], er2,
+                            [outs[j] if j in er2 else None for j in range(14)], chunk, 0,
+                            torch.cuda.current_stream().cuda_stream)
+    del g, g2
+    torch.cuda.synchronize()
+    clay_amd.release_captured(0)
