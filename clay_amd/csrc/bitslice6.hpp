@@ -1,7 +1,7 @@
 // bitslice6.hpp -- v6 bit-sliced encode for (10,4,13): 128-byte runs per sub-chunk row.
 //
 // Why: the v4 kernel (64-byte tiles) runs at the ceiling of its own access pattern --
-// tools/dmabench2 shows 64-byte runs per sub-chunk row cap the LDS-DMA sweep at ~3.8 TB/s
+// bench_tools/run_width_probe shows 64-byte runs per sub-chunk row cap the LDS-DMA sweep at ~3.8 TB/s
 // and 128-byte runs reach ~4.6 TB/s (reads + parity stores, no math).  v4's accumulators
 // (64 KiB LDS per 64-byte tile) leave no room to double the tile, so v6 re-partitions:
 //
