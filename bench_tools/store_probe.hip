@@ -94,6 +94,49 @@ __global__ __launch_bounds__(512) void k_parity_order(uint8_t *par, uint32_t sc,
     }
 }
 
+// Variants of the parity pattern (random data): the same 1,024 rows x sc bytes, a tile = W bytes of
+// every row, 512 threads per workgroup, grid 256 (one per CU).
+//   ORDER 0: XCD-blocked (XCD x owns a contiguous byte region, its 32 workgroups round robin)
+//   ORDER 1: chip round robin (tile t -> workgroup t % 256: the chip covers 256 adjacent tiles)
+//   ORDER 2: one contiguous byte range per workgroup
+//   ROWS: 0 = wave w writes rows 128w.. (the encode), 1 = step i of all 8 waves writes 32
+//   consecutive rows, 2 = every wave writes 1 row at a time (W/1024 rows per instruction group)
+template <int W, int ORDER, int ROWS>
+__global__ __launch_bounds__(512) void k_parity_var(uint8_t *par, uint32_t sc, uint64_t chunk) {
+    const uint32_t ntiles = sc / W, b = blockIdx.x, G = gridDim.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int RPI = 1024 / W;                    // rows per wave instruction (W <= 1024)
+    constexpr int NI = 1024 / 8 / RPI;               // instructions per wave per tile
+    const int lr = lane / (64 / RPI), lof = (lane % (64 / RPI)) * 16;
+    v4u st = seed_of(threadIdx.x + blockIdx.x * 512u);
+    uint32_t t0, tstep, tn;
+    if (ORDER == 0) {
+        const uint32_t tpx = (ntiles + 7) / 8, nsl = G / 8;
+        t0 = (b & 7) * tpx + (b >> 3);
+        tstep = nsl;
+        tn = (b & 7) * tpx + tpx < ntiles ? (b & 7) * tpx + tpx : ntiles;
+    } else if (ORDER == 1) {
+        t0 = b;
+        tstep = G;
+        tn = ntiles;
+    } else {
+        const uint32_t per = (ntiles + G - 1) / G;
+        t0 = b * per;
+        tstep = 1;
+        tn = t0 + per < ntiles ? t0 + per : ntiles;
+    }
+    for (uint32_t t = t0; t < tn; t += tstep) {
+        const uint32_t b0 = t * W;
+        for (int i = 0; i < NI; i++) {
+            int row;
+            if (ROWS == 0) row = (wave * NI + i) * RPI + lr;
+            else row = (i * 8 + wave) * RPI + lr;
+            uint8_t *p = par + uint64_t(row >> 8) * chunk + uint64_t(row & 255) * sc + b0 + lof;
+            *reinterpret_cast<v4u *>(p) = make_val<2>(st, row);
+        }
+    }
+}
+
 template <class F>
 static float timeit(F &&launch, int reps = 16) {
     hipEvent_t e0, e1;
@@ -180,6 +223,17 @@ int main(int argc, char **argv) {
                     if (data == 2) k_parity_order<2><<<256, 512>>>(b, sc, chunk);
                 }));
         }
+    }
+    if (all || !strcmp(only, "pvar")) {
+        const uint32_t sc = 419432;
+        const uint64_t chunk = uint64_t(sc) * 256;
+        const double pb = 4.0 * chunk;
+#define PV(W, O, R)                                                                                 \
+    snprintf(nm, sizeof nm, "parity W%d order%d rows%d", W, O, R);                                \
+    rep(nm, pb, timeit([&] { k_parity_var<W, O, R><<<256, 512>>>(b, sc, chunk); }));
+        PV(256, 0, 0) PV(256, 0, 1) PV(256, 1, 0) PV(256, 1, 1) PV(256, 2, 0) PV(256, 2, 1)
+        PV(512, 0, 0) PV(512, 0, 1) PV(512, 1, 0) PV(512, 1, 1) PV(512, 2, 0)
+        PV(1024, 0, 0) PV(1024, 0, 1) PV(1024, 1, 0) PV(1024, 1, 1) PV(1024, 2, 0)
     }
     return 0;
 }

@@ -105,6 +105,20 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
+    if (argc > 2 && argv[2][0] == 'm') {  // tile map A/B (PROBE bit 2048 = chip round robin)
+        printf("sc %u tile map (XCD-blocked vs chip round robin), back-to-back\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b full, XCD-blocked", run_b2b<4, 0>(a, 200));
+            rep("b2b full, chip RR", run_b2b<4, 2048>(a, 200));
+            rep("b2b memory only, XCD-blocked", run_b2b<4, 1>(a, 200));
+            rep("b2b memory only, chip RR", run_b2b<4, 2049>(a, 200));
+            rep("b2b stores only, XCD-blocked", run_b2b<4, 3>(a, 200));
+            rep("b2b stores only, chip RR", run_b2b<4, 2051>(a, 200));
+            rep("b2b reads only, XCD-blocked", run_b2b<4, 5>(a, 200));
+            rep("b2b reads only, chip RR", run_b2b<4, 2053>(a, 200));
+        }
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'x') {  // CSE folds A/B (PROBE bit 1024 = without)
         printf("sc %u cse folds\n", sc);
         for (int rr = 0; rr < 3; rr++) {

@@ -282,6 +282,8 @@ static Tuning read_tuning() {
     t.host_piece = size_t(ival("CLAY_HOST_PIECE_MB", 256)) << 20;
     t.host_streams = int(ival("CLAY_HOST_STREAMS", 2));
     t.decode_probe = int(ival("CLAY_DECODE_PROBE", 0));
+    const long long ring = ival("CLAY_DECODE_RING", 10);
+    t.decode_ring = uint32_t(ring >= 6 && ring <= 10 ? ring : 10);
     return t;
 }
 // namespace-scope: initialised when the library is loaded, before any ABI call

@@ -34,7 +34,16 @@ struct DecArgs {
     // split mode (k_stream_syn + k_stream_solve): S of tile b0 / 64 at ws + (b0 / 64) * 64 KiB,
     // layout [check j][layer z][64 B] (the S/C region of the fused kernel)
     uint8_t *ws;
+    // local decode (k_stream_local): bit position of section y's layer digit in the column c
+    // (a permutation of 0, 2, 4 over the sections != G; section g2's digit at 0, so its lines
+    // are lanes l, l ^ 8, l ^ 16, l ^ 24 of one wave); g2 = the section of the one erasure
+    // outside section G (-1: none), x2 its digit
+    uint32_t csh[4];
+    int32_t g2;
+    uint32_t x2;
 };
+// local decode: v_perm table of det^-1 = (1 + gamma^2)^-1 (pair inversion, transforms.rs:108-125)
+constexpr int kDecDetInv = 80;
 constexpr int kDecOrder = 640;
 // split solve: correction pairs (uint16 layer | Y << 8 | X << 10: C(e_Y, z[Y:=X]) feeds layer z)
 // from dword kDecPairs; at most 768 (4 erasures: 108 x 3 + 54 x 6 + 12 x 9 + 12)

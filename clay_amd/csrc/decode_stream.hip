@@ -10,6 +10,7 @@
 #include <utility>
 
 #include "stream_decode.hpp"
+#include "stream_local.hpp"
 #include "tuning.hpp"
 
 namespace clay {
@@ -60,6 +61,46 @@ static hipError_t launch_split(const bs::DecArgs &a, hipStream_t stream, int dev
     b.region = (nst + 7) / 8 * 128;
     bs::k_stream_solve<KD, G, SPROBE><<<dim3(b.nslots * 8), dim3(1024), bs::kSolveLds, stream>>>(b);
     return hipGetLastError();
+}
+
+template <int KD, int G>
+static hipError_t launch_local(const bs::DecArgs &a, hipStream_t stream, int dev) {
+    using Kn = bs::StreamDec<KD, G>;
+    static std::mutex mu;
+    static std::set<int> done;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!done.count(dev)) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_local<KD, G>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
+            if (e != hipSuccess) return e;
+            done.insert(dev);
+        }
+    }
+    bs::k_stream_local<KD, G><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+    return hipGetLastError();
+}
+
+// the local decode (stream_local.hpp): erasures in section g plus at most one other section
+hipError_t launch_stream_local_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream, int dev) {
+    if (kd == 10) {
+        switch (g) {
+        case 0: return launch_local<10, 0>(a, stream, dev);
+        case 1: return launch_local<10, 1>(a, stream, dev);
+        case 2: return launch_local<10, 2>(a, stream, dev);
+        case 3: return launch_local<10, 3>(a, stream, dev);
+        default: break;
+        }
+    } else if (kd == 9) {
+        switch (g) {
+        case 0: return launch_local<9, 0>(a, stream, dev);
+        case 1: return launch_local<9, 1>(a, stream, dev);
+        case 2: return launch_local<9, 2>(a, stream, dev);
+        case 3: return launch_local<9, 3>(a, stream, dev);
+        default: break;
+        }
+    }
+    return hipErrorInvalidValue;
 }
 
 // a.ws != nullptr: split decode (two launches), else the fused single-launch kernel

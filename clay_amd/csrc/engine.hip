@@ -737,6 +737,11 @@ static Error lease_acquire(DevState &ds, size_t bytes, hipStream_t st, Lease **o
             }
         }
     }
+    if (!best && cap)  // no allocation while capturing (it would invalidate the capture)
+        return make_error(CLAY_ERR_DEVICE, bytes, 0, 0,
+                          "no idle workspace of %zu bytes for a stream capture: call clay_reserve_workspace before "
+                          "capturing (a captured call keeps its workspace until clay_release_captured)",
+                          bytes);
     if (!best) {
         auto l = std::make_unique<Lease>();
         CLAY_HIP(hipMalloc(&l->d, std::max<size_t>(bytes, 256)));
@@ -1092,7 +1097,8 @@ static int align_of(uintptr_t p) {
 }
 
 // Executor selection (clay_set_exec_mode): process-wide, read without locks.
-enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3, kExecStreamFused = 4 };  // see clay_set_exec_mode
+enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3, kExecStreamFused = 4,
+              kExecStreamLocal = 5 };  // see clay_set_exec_mode
 static std::atomic<int> g_exec_mode{kExecAuto};
 static size_t tex_lds_budget() { return tuning().texec_lds; }
 // Lane width of the tile-fused executor for a plan (0 = not eligible): the widest of
@@ -1756,11 +1762,13 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
 // outputs of erased nodes, nullptr if not wanted).
 hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
 
+// Shared by the streaming decodes: pattern checks, RS rows used, H_K^-1, the v_perm tables of
+// its rows and of A_i = H_K^-1 gamma H_i, the node loads of a tile.  *ok = false: not eligible
+// (per_sec_max: the most erasures one y-section may hold).
 template <int KD>
-static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &prop, const uint8_t *const *cin,
-                                  uint8_t *const *cout, const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream,
-                                  bool split, bool *done) {
-    *done = false;
+static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const *cout, const std::vector<uint8_t> &erased,
+                       size_t sc, int per_sec_max, bs::DecArgs &a, std::vector<uint32_t> &tabs, bool *ok) {
+    *ok = false;
     const clay_code_t &c = cs.code;
     using S = bs::Shape<KD, 4>;
     if (int(c.k) != KD || c.m != 4 || c.q != 4 || c.t != 4 || c.q * c.t != 16) return Error{};
@@ -1775,7 +1783,7 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         }
     if (E.empty() || E.size() > 4) return Error{};
     for (int y = 0; y < 4; y++)
-        if (per_sec[y] > 1) return Error{};  // PFT pair inside a round: not in this kernel
+        if (per_sec[y] > per_sec_max) return Error{};
     for (int i = 0; i < 16; i++) {
         if (cin[i] && reinterpret_cast<uintptr_t>(cin[i]) % 8) return Error{};
         if (cout[i] && reinterpret_cast<uintptr_t>(cout[i]) % 8) return Error{};
@@ -1784,7 +1792,8 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         for (int i = 0; i < S::K; i++)
             if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
                 return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    bs::DecArgs a{};
+    a = bs::DecArgs{};
+    a.g2 = -1;
     // RS rows used: the first 12 present shards (reconstruct, decode.rs:374); K = the rest
     uint32_t used = 0;
     int nused = 0;
@@ -1806,7 +1815,7 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         for (int j = 0; j < 4; j++) hk[pchk * 4 + j] = Hc(pchk, Kset[j]);
     if (!gf_invert(hk, 4, hinv)) return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "singular RS check submatrix");
     a.ne = uint32_t(E.size());
-    std::vector<uint32_t> tabs(bs::kDecTabWords, 0);
+    tabs.assign(bs::kDecTabWords, 0);
     for (int i = 0; i < 16; i++) a.rix[i] = -1;
     for (size_t r = 0; r < E.size(); r++) {
         const int e = E[r];
@@ -1822,7 +1831,7 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         }
     }
     a.used = used;
-    const uint32_t R = 10;
+    const uint32_t R = tuning().decode_ring;  // 10 unless a measurement sets CLAY_DECODE_RING
     uint32_t n[4] = {0, 0, 0, 0}, nt = 0;
     for (int y = 0; y < 4; y++) {
         a.sec_off[y] = nt;
@@ -1843,6 +1852,41 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         if (n[y] > R || (y < 3 && n[y] + n[y + 1] > R)) return Error{};
     if (R < 5) return Error{};  // S/C region (4 buffers) + the phase-B table buffer
     a.ring = R;
+    a.sc = sc;
+    a.region = uint32_t(((sc + 7) / 8 + 63) / 64 * 64);
+    *ok = true;
+    return Error{};
+}
+
+// the pattern's tables: uploaded once per (table contents, device), cached with the code
+static Error dec_tables(CodeState &cs, const DevProps &prop, const std::vector<uint32_t> &tabs, hipStream_t stream,
+                        const uint32_t **out) {
+    std::lock_guard<std::mutex> lk(cs.mu);
+    auto key = std::make_pair(std::vector<uint32_t>(tabs), prop.dev);
+    auto it = cs.dtabs.find(key);
+    if (it == cs.dtabs.end()) {
+        if (capturing(stream)) return not_prepared("streaming-decode pattern table");
+        const uint32_t *d = nullptr;
+        Error ue = upload_vec(tabs, &d);
+        if (ue) return ue;
+        it = cs.dtabs.emplace(key, d).first;
+    }
+    *out = it->second;
+    return Error{};
+}
+
+template <int KD>
+static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &prop, const uint8_t *const *cin,
+                                  uint8_t *const *cout, const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream,
+                                  bool split, bool *done) {
+    *done = false;
+    bs::DecArgs a;
+    std::vector<uint32_t> tabs;
+    bool ok = false;
+    // two erasures in one section need a PFT pair inside a round: not in these kernels
+    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
+    if (e || !ok) return e;
+    const uint32_t used = a.used;
     // phase-B layer order: by iscore level (red erased sections), then by the set of red
     // sections (uniform corrections per wave), rounds of <= 128 layers of one level
     std::vector<std::pair<uint32_t, int>> lay;
@@ -1893,24 +1937,10 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
         }
         a.pstart[nr] = np;
     }
-    a.sc = sc;
-    a.region = uint32_t(((sc + 7) / 8 + 63) / 64 * 64);
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
     a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
-    // the pattern's tables: uploaded once per (pattern, device), cached with the code
-    {
-        std::lock_guard<std::mutex> lk(cs.mu);
-        auto key = std::make_pair(std::vector<uint32_t>(tabs), prop.dev);
-        auto it = cs.dtabs.find(key);
-        if (it == cs.dtabs.end()) {
-            if (capturing(stream)) return not_prepared("streaming-decode pattern table");
-            const uint32_t *d = nullptr;
-            Error ue = upload_vec(tabs, &d);
-            if (ue) return ue;
-            it = cs.dtabs.emplace(key, d).first;
-        }
-        a.tabs = it->second;
-    }
+    e = dec_tables(cs, prop, tabs, stream, &a.tabs);
+    if (e) return e;
     // split decode (k_stream_syn + k_stream_solve, S through a pooled workspace of 64 KiB per
     // 64-byte tile) unless exec mode "stream-fused" selects the fused single-launch kernel
     LeaseGuard ws(ds, stream);
@@ -1922,6 +1952,55 @@ static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &p
     CLAY_HIP(launch_stream_decode_kernel(KD, a, stream, prop.dev));
     t_last_launches += split ? 2 : 1;
     t_last_exec = split ? "stream-split" : "stream";
+    *done = true;
+    return Error{};
+}
+
+hipError_t launch_stream_local_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
+
+// Local decode (stream_local.hpp): erasures in one y-section G (any number) plus at most one
+// erasure in one other section g2 -- every iscore dependency inside a wave, one launch, no
+// workspace.  G = the section with the most erasures; section g2's digit goes to bits 0-1 of
+// the lane column.
+template <int KD>
+static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
+                                 const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream, bool *done) {
+    *done = false;
+    int per_sec[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16 && i < int(erased.size()); i++) per_sec[i / 4] += erased[i] ? 1 : 0;
+    int G = 0, nsec = 0;
+    for (int y = 0; y < 4; y++) {
+        if (per_sec[y] > per_sec[G]) G = y;
+        nsec += per_sec[y] ? 1 : 0;
+    }
+    if (nsec == 0 || nsec > 2) return Error{};
+    int g2 = -1;
+    for (int y = 0; y < 4; y++)
+        if (y != G && per_sec[y]) {
+            if (per_sec[y] > 1) return Error{};  // two sections with several erasures: rounds needed
+            g2 = y;
+        }
+    bs::DecArgs a;
+    std::vector<uint32_t> tabs;
+    bool ok = false;
+    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 4, a, tabs, &ok);
+    if (e || !ok) return e;
+    // column digits: section g2 (if any) at bits 0-1, the others above in section order
+    {
+        uint32_t sh = 4;
+        for (int y = 0; y < 4; y++)
+            if (y != G) a.csh[y] = y == g2 ? 0u : (sh -= 2) + 2;
+    }
+    a.g2 = g2;
+    if (g2 >= 0) a.x2 = uint32_t(__builtin_ctz(a.emask[g2]));
+    perm_table(gamma_det_inv(), &tabs[bs::kDecDetInv * 8]);  // (1 + gamma^2)^-1, transforms.rs:108-125
+    const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
+    a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
+    e = dec_tables(cs, prop, tabs, stream, &a.tabs);
+    if (e) return e;
+    CLAY_HIP(launch_stream_local_kernel(KD, G, a, stream, prop.dev));
+    t_last_launches += 1;
+    t_last_exec = "stream-local";
     *done = true;
     return Error{};
 }
@@ -1978,7 +2057,11 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     const int xmode = g_exec_mode.load(std::memory_order_relaxed);
     size_t n_erased = 0;
     for (size_t in = 0; in < tn; in++) n_erased += erased[in] && !(in >= c.k && in < c.k + c.nu) ? 1 : 0;
-    if ((xmode == kExecStream || xmode == kExecStreamFused || (xmode == kExecAuto && n_erased >= 3)) && tn == 16) {
+    // local decode (erasures in one section plus at most one other, stream_local.hpp): auto and
+    // exec mode "stream-local"
+    const bool try_local = xmode == kExecAuto || xmode == kExecStreamLocal;
+    const bool try_split = xmode == kExecStream || xmode == kExecStreamFused || (xmode == kExecAuto && n_erased >= 3);
+    if ((try_local || try_split) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};
         for (size_t i = 0; i < c.n; i++) {
@@ -1989,11 +2072,18 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         bool done = false;
         const DevProps &prop = dev_props(dev);
         const size_t sc = chunk / c.sub_chunk_no;
-        const bool split = xmode != kExecStreamFused;
         hipStream_t st = static_cast<hipStream_t>(stream);
-        if (c.k == 10) e = launch_stream_decode<10>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
-        else if (c.k == 9) e = launch_stream_decode<9>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
-        if (e || done) return e;
+        if (try_local) {
+            if (c.k == 10) e = launch_stream_local<10>(cs, prop, cin, cout, erased, sc, st, &done);
+            else if (c.k == 9) e = launch_stream_local<9>(cs, prop, cin, cout, erased, sc, st, &done);
+            if (e || done) return e;
+        }
+        if (try_split) {
+            const bool split = xmode != kExecStreamFused;
+            if (c.k == 10) e = launch_stream_decode<10>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
+            else if (c.k == 9) e = launch_stream_decode<9>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
+            if (e || done) return e;
+        }
     }
     return run_plan(cs, *plan, dev, *ds, static_cast<hipStream_t>(stream), P, chunk / c.sub_chunk_no, chunk);
 }
@@ -2258,7 +2348,8 @@ int clay_set_encode_path(int mode) {
     return prev;
 }
 int clay_set_exec_mode(int mode) {
-    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream && mode != kExecStreamFused)
+    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream && mode != kExecStreamFused &&
+        mode != kExecStreamLocal)
         return -1;
     return g_exec_mode.exchange(mode);
 }

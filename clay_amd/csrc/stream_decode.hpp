@@ -90,6 +90,14 @@ struct StreamDec {
         for (int k = 0; k < 3; k++) z += ((c >> (2 * (2 - k))) & 3u) * wt(cd(k));
         return z;
     }
+    // the same with the column digits at run-time positions a.csh[y] (k_stream_local)
+    __device__ static uint32_t layer0_rt(const DecArgs &a, uint32_t c) {
+        uint32_t z = 0;
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+            if (y != G) z += ((c >> a.csh[y]) & 3u) * wt(y);
+        return z;
+    }
     // byte offset of row (c, g) within a node buffer
     __device__ static uint32_t row(uint32_t c, uint32_t g) { return c * 256u + ((g ^ (c & 3u)) << 6); }
 
@@ -165,6 +173,16 @@ struct StreamDec {
             L.off[j] = (layer0(cc) + g * wt(G)) * sc + L.pc16;
         }
     }
+    __device__ static void loader_init_rt(Loader &L, const DecArgs &a, int li, int lane) {
+        const uint32_t k = uint32_t(lane), sc = uint32_t(a.sc);
+        L.pc16 = (k & 3u) * 16u;
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            const uint32_t cc = uint32_t(li * BPL + j) * 4u + (k >> 4);
+            const uint32_t g = ((k >> 2) & 3u) ^ (k >> 4);
+            L.off[j] = (layer0_rt(a, cc) + g * wt(G)) * sc + L.pc16;
+        }
+    }
     __device__ static void issue(const DecArgs &a, const Loader &L, uint32_t lds_buf, const uint8_t *node, Tile t,
                                  int li) {
         lds_buf = __builtin_amdgcn_readfirstlane(lds_buf);
@@ -187,7 +205,8 @@ struct StreamDec {
     // ---------------- phase A: one step per section (decode.rs:260-329, transforms.rs:42-89) ----------------
     // S (4 checks x 8 planes, the lane's 4 layers x 8 positions) += sum_i H_i U'(i) + H_e Out(e);
     // section Y's alive nodes are loads qbase + sec_off[Y] .. of the ring (buffer = load % ring).
-    template <int PROBE>
+    // RT (k_stream_local): column digits at a.csh[y], and any number of erased nodes in section G
+    template <int PROBE, bool RT = false>
     __device__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
                                    uint32_t (&S)[32], uint32_t R) {  // R: ring depth (node buffers)
         sfor<4>([&](auto yc) BS_INL {
@@ -202,7 +221,7 @@ struct StreamDec {
                 return smem + ((qbase + q) % R) * BUF;
             };
             if constexpr (Y != G) {
-                constexpr int sh = csh(Y);
+                const uint32_t sh = RT ? a.csh[Y] : uint32_t(csh(Y));
                 const uint32_t cy = (c >> sh) & 3u;
                 const bool comp_alive = (aliveY >> cy) & 1u;
                 const uint8_t *cbuf = comp_alive ? buf_of(cy) : smem;
@@ -251,7 +270,24 @@ struct StreamDec {
                         for (int w = 0; w < 8; w++) o[X][w] = 0;
                     }
                 });
-                if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
+                if constexpr (RT) {
+                    // every erased node (G, A): Out((G, A), slot g) = gamma * C((G, g), slot A), 0 at
+                    // slot A and where (G, g) has no data (erased: a both-erased pair, inverted later)
+                    const uint32_t emG = a.emask[G];
+                    sfor<4>([&](auto ac) BS_INL {
+                        constexpr int A = decltype(ac)::value;
+                        if (!((emG >> A) & 1u)) return;
+                        uint32_t v[8];
+#pragma unroll
+                        for (int g = 0; g < 4; g++) {
+                            v[2 * g] = g == A ? 0u : gf_xt(o[g][2 * A]);
+                            v[2 * g + 1] = g == A ? 0u : gf_xt(o[g][2 * A + 1]);
+                        }
+                        transpose8(v);
+                        fold<4 * G + A, false>(v, S);
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                } else if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
                     uint32_t v[8];
                     sfor<4>([&](auto gc) BS_INL {
                         constexpr int g = decltype(gc)::value;

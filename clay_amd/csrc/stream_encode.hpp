@@ -82,6 +82,21 @@ struct StreamMap {
     }
 };
 
+// Chip round robin (probe): full tile t -> workgroup t % G (the whole chip covers G adjacent
+// tiles at a time), the partial last tile to workgroup nfull % G.
+struct ChipMap {
+    uint32_t b, G, nfull, pend, sc;
+    __device__ ChipMap(uint32_t sc_, uint32_t b_, uint32_t G_) : b(b_), G(G_), nfull(sc_ / 256u), sc(sc_) {
+        pend = (sc_ % 256u) && (nfull % G_) == b_ ? 1u : 0u;
+    }
+    __device__ int ntile() const { return int((nfull > b ? (nfull - b + G - 1) / G : 0u) + pend); }
+    __device__ StreamTile tile(int k, uint32_t, uint32_t) const {
+        const uint32_t t = b + uint32_t(k) * G;
+        if (t < nfull) return {t * 256u, t * 256u + 256u};
+        return {nfull * 256u, sc};
+    }
+};
+
 // CPL / CPS: cache policy of the LDS-DMA loads / parity stores (0 default, 1 nt, 2 sc1);
 // CSE: RS folds through compile-time common subexpressions (xor_cse.hpp)
 template <int KD, int LOADERS, int CPL = 0, int CPS = 0, bool CSE = true>
@@ -387,7 +402,7 @@ struct StreamEnc {
 // (no CSE: bench_tools/stream_probe x, 0.350 vs 0.353 ms full, 0.257 vs 0.281 math + stores),
 // 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1, 32 = the group whose
 // outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
-// across workgroups; only meaningful with bit 1).
+// across workgroups; only meaningful with bit 1), 2048 = chip round-robin tile map (ChipMap).
 template <int KD, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
     using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3, ((PROBE >> 10) & 1) == 0>;
@@ -395,7 +410,10 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, ns = a.nslots;
-    const StreamMap tm(uint32_t(a.sc), a.tiles_per_xcd, ns, xcd, slot);
+    const auto tm = [&] {
+        if constexpr ((PROBE & 2048) != 0) return ChipMap(uint32_t(a.sc), blockIdx.x, gridDim.x);
+        else return StreamMap(uint32_t(a.sc), a.tiles_per_xcd, ns, xcd, slot);
+    }();
     const int ntile = tm.ntile();
     if (ntile == 0) return;  // uniform per workgroup
     const int nsteps = ntile * Kn::STEPS;

@@ -33,6 +33,9 @@ struct Tuning {
     int host_streams = 2;                   // CLAY_HOST_STREAMS
     // probe library only (libclay_amd_probe.so): decode kernel parts to skip
     int decode_probe = 0;        // CLAY_DECODE_PROBE
+    // streaming decodes: LDS node buffers of the ring (6..10; the split syn kernel and the local
+    // kernel use one less, the last holds the tables)
+    uint32_t decode_ring = 10;   // CLAY_DECODE_RING
 };
 
 // The knobs as read at load time.

@@ -271,7 +271,10 @@ int clay_set_encode_path(int mode);
  *                per-level executor; decodes of >= 3 erasures of q = 4, t = 4 codes
  *                ((10,4,13), (9,4,12)) in distinct y-sections with sc % 8 == 0, sc >= 512 run
  *                the split streaming decode (k_stream_syn + k_stream_solve, last path
- *                "stream-split")
+ *                "stream-split"); decodes of those codes whose erasures lie in one y-section
+ *                plus at most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4},
+ *                {0,1,2,3}, ...) run the single-launch local decode (k_stream_local,
+ *                "stream-local")
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
  *   (auto and stream: repair of (9,3,11), (10,4,13), (4,2,5) from all n - 1 other nodes runs
@@ -281,6 +284,7 @@ int clay_set_encode_path(int mode);
  *   3 stream  -- every eligible decode of q = 4, t = 4 codes (any erasure count) on the split
  *                streaming decode ("stream-split"); everything else as auto
  *   4 stream-fused -- as stream, but on the fused single-launch k_stream_decode ("stream")
+ *   5 stream-local -- every decode the local kernel takes on it ("stream-local"); else as auto
  * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
  * (planner and executor tuning) are read once when the library is loaded.
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
@@ -288,7 +292,7 @@ int clay_set_encode_path(int mode);
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
  * "tile" (k_texec), "grouped" (k_gexec), "stream-split" (k_stream_syn + k_stream_solve),
- * "stream" (k_stream_decode), "bs-repair-stream" (k_bs_repair_stream), "bs-repair"
+ * "stream" (k_stream_decode), "stream-local" (k_stream_local), "bs-repair-stream" (k_bs_repair_stream), "bs-repair"
  * (k_bs_repair) or "none". */
 const char *clay_last_exec_path(void);
 

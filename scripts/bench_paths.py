@@ -138,6 +138,11 @@ if __name__ == "__main__":
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0])),
             ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
             ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),
+            # same-section and mixed patterns (the local decode in auto)
+            ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1])),
+            ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4])),
+            ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 2, 3])),
+            ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [12])),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 0)),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 11)),
             ("repair", lambda: repair_cfg(10, 4, 13, 107_374_592, 0)),

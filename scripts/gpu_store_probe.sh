@@ -5,10 +5,10 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" && mkdir -p gpurun_out
 TAG=${1:-store}
-timeout -k 10 300 ./bench_tools/store_probe > gpurun_out/${TAG}_store_probe.txt 2>&1 || { echo "store_probe failed"; tail -5 gpurun_out/${TAG}_store_probe.txt; exit 1; }
+timeout -k 10 300 ./bench_tools/store_probe ${PROBE_MODE:-all} > gpurun_out/${TAG}_store_probe.txt 2>&1 || { echo "store_probe failed"; tail -5 gpurun_out/${TAG}_store_probe.txt; exit 1; }
 cat gpurun_out/${TAG}_store_probe.txt
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_memset_trace" -o memset -- "$R/bench_tools/store_probe" memset > "$R/gpurun_out/${TAG}_memset_trace.log" 2>&1 || { echo "trace failed"; tail -20 "$R/gpurun_out/${TAG}_memset_trace.log"; exit 1; }
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_memset_trace" -o memset --output-format csv -- "$R/bench_tools/store_probe" memset > "$R/gpurun_out/${TAG}_memset_trace.log" 2>&1 || { echo "trace failed"; tail -20 "$R/gpurun_out/${TAG}_memset_trace.log"; exit 1; }
 f=$(find "$R/gpurun_out/${TAG}_memset_trace" -name "*kernel_trace.csv" | head -1)
 python3 - "$f" <<'EOF'
 import csv, sys, collections

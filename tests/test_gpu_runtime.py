@@ -392,6 +392,7 @@ def test_capture_arena_reclaimed(oracle_mod, torch_cuda):
     st.synchronize()
 
     def capture():
+        c.reserve_workspace(n * chunk)  # each captured call keeps its workspace: one idle lease per capture
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=st):
             c.encode_device_batch(dl, pl, n, chunk, 0, torch.cuda.current_stream().cuda_stream)
