@@ -109,7 +109,7 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
-_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-fused": 4, "stream-local": 5}
+_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-fused": 4, "stream-local": 5, "stream-fused2": 6}
 
 
 def set_exec_mode(mode: str) -> str:

@@ -11,6 +11,7 @@
 
 #include "stream_decode.hpp"
 #include "stream_local.hpp"
+#include "stream_fused2.hpp"
 #include "tuning.hpp"
 
 namespace clay {
@@ -100,6 +101,43 @@ hipError_t launch_stream_local_kernel(int kd, int g, const bs::DecArgs &a, hipSt
         default: break;
         }
     }
+    return hipErrorInvalidValue;
+}
+
+template <int KD, int PROBE = 0>
+static hipError_t launch_f2(const bs::DecArgs &a, hipStream_t stream, int dev) {
+    static std::mutex mu;
+    static std::set<int> done;
+    const int lds = int(a.ring + 4) * bs::kDecBuf;  // ring + S/C region
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!done.count(dev)) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_fused2<KD, 3, PROBE>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            done.insert(dev);
+        }
+    }
+    bs::k_stream_fused2<KD, 3, PROBE><<<dim3(a.nslots * 8), dim3(bs::StreamDec<KD, 3>::BLOCK), lds, stream>>>(a);
+    return hipGetLastError();
+}
+
+// the fused decode v2 (stream_fused2.hpp): one erasure per y-section
+hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev) {
+#ifdef CLAY_DECODE_PROBES
+    const int probe = tuning().decode_probe;
+    if (kd == 10 && probe >= 31 && probe <= 39) {  // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only
+        switch (probe) {
+        case 31: return launch_f2<10, 1>(a, stream, dev);
+        case 32: return launch_f2<10, 2>(a, stream, dev);
+        case 34: return launch_f2<10, 4>(a, stream, dev);
+        case 35: return launch_f2<10, 13>(a, stream, dev);
+        default: break;
+        }
+    }
+#endif
+    if (kd == 10) return launch_f2<10>(a, stream, dev);
+    if (kd == 9) return launch_f2<9>(a, stream, dev);
     return hipErrorInvalidValue;
 }
 

@@ -1098,7 +1098,7 @@ static int align_of(uintptr_t p) {
 
 // Executor selection (clay_set_exec_mode): process-wide, read without locks.
 enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3, kExecStreamFused = 4,
-              kExecStreamLocal = 5 };  // see clay_set_exec_mode
+              kExecStreamLocal = 5, kExecStreamFused2 = 6 };  // see clay_set_exec_mode
 static std::atomic<int> g_exec_mode{kExecAuto};
 static size_t tex_lds_budget() { return tuning().texec_lds; }
 // Lane width of the tile-fused executor for a plan (0 = not eligible): the widest of
@@ -2005,6 +2005,55 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
     return Error{};
 }
 
+hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
+
+// Fused decode v2 (stream_fused2.hpp): one erasure per y-section, one launch, rounds of tile k-1
+// on the loader waves while tile k streams.  Ring of 6 node buffers + the S/C region.
+template <int KD>
+static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
+                                  const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream, bool *done) {
+    *done = false;
+    bs::DecArgs a;
+    std::vector<uint32_t> tabs;
+    bool ok = false;
+    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
+    if (e || !ok) return e;
+    constexpr uint32_t RB = 6;
+    for (int y = 0; y < 4; y++) {
+        const uint32_t ny = a.sec_off[y + 1] - a.sec_off[y];
+        const uint32_t nn = y < 3 ? a.sec_off[y + 2] - a.sec_off[y + 1] : 0u;
+        if (ny > RB || ny + nn > RB) return Error{};
+    }
+    a.ring = RB;
+    // per (level, Y, X): target layers z of that iscore level, red in section Y, X != x_e(Y) used
+    uint8_t *zl = reinterpret_cast<uint8_t *>(tabs.data()) + bs::kDecZList;
+    uint32_t nz = 0;
+    for (uint32_t lv = 0; lv < 4; lv++)
+        for (uint32_t gi = 0; gi < 16; gi++) {
+            a.gstart[lv * 16 + gi] = uint16_t(nz);
+            const uint32_t Y = gi >> 2, X = gi & 3u;
+            if (!a.emask[Y] || ((a.emask[Y] >> X) & 1u) || !((a.used >> (4 * Y + X)) & 1u)) continue;
+            const uint32_t xe = uint32_t(__builtin_ctz(a.emask[Y]));
+            for (uint32_t z = 0; z < 256; z++) {
+                uint32_t level = 0;
+                for (int y = 0; y < 4; y++) level += (a.emask[y] >> ((z >> (2 * (3 - y))) & 3u)) & 1u;
+                if (level != lv + 1 || ((z >> (2 * (3 - Y))) & 3u) != xe) continue;
+                if (nz >= 768) return Error{};
+                zl[nz++] = uint8_t(z);
+            }
+        }
+    a.gstart[64] = uint16_t(nz);
+    const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
+    a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
+    e = dec_tables(cs, prop, tabs, stream, &a.tabs);
+    if (e) return e;
+    CLAY_HIP(launch_stream_fused2_kernel(KD, a, stream, prop.dev));
+    t_last_launches += 1;
+    t_last_exec = "stream-fused2";
+    *done = true;
+    return Error{};
+}
+
 static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
                                 uint8_t *const *outs, size_t chunk, int dev, void *stream) {
     Error e = check_code(code);
@@ -2061,7 +2110,8 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     // exec mode "stream-local"
     const bool try_local = xmode == kExecAuto || xmode == kExecStreamLocal;
     const bool try_split = xmode == kExecStream || xmode == kExecStreamFused || (xmode == kExecAuto && n_erased >= 3);
-    if ((try_local || try_split) && tn == 16) {
+    const bool try_f2 = xmode == kExecStreamFused2;
+    if ((try_local || try_split || try_f2) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};
         for (size_t i = 0; i < c.n; i++) {
@@ -2076,6 +2126,11 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         if (try_local) {
             if (c.k == 10) e = launch_stream_local<10>(cs, prop, cin, cout, erased, sc, st, &done);
             else if (c.k == 9) e = launch_stream_local<9>(cs, prop, cin, cout, erased, sc, st, &done);
+            if (e || done) return e;
+        }
+        if (try_f2) {
+            if (c.k == 10) e = launch_stream_fused2<10>(cs, prop, cin, cout, erased, sc, st, &done);
+            else if (c.k == 9) e = launch_stream_fused2<9>(cs, prop, cin, cout, erased, sc, st, &done);
             if (e || done) return e;
         }
         if (try_split) {
@@ -2349,7 +2404,7 @@ int clay_set_encode_path(int mode) {
 }
 int clay_set_exec_mode(int mode) {
     if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream && mode != kExecStreamFused &&
-        mode != kExecStreamLocal)
+        mode != kExecStreamLocal && mode != kExecStreamFused2)
         return -1;
     return g_exec_mode.exchange(mode);
 }

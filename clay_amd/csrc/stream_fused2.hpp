@@ -1,0 +1,204 @@
+// stream_fused2.hpp -- single-launch decode for q = 4, t = 4 codes with one erasure in each of up
+// to four y-sections (the BASELINE worst case {0,4,8,12}): every survivor byte read from HBM
+// once, every output byte written once, and the latency-bound iscore rounds (decode.rs:196-254)
+// of tile k-1 run on other waves while tile k streams.
+//
+// Why not k_stream_decode (the fused kernel of stream_decode.hpp)?  There the compute waves run
+// phase B themselves and its S/C region aliases ring buffers, so every tile drains the load
+// pipeline (measured: memory + phase A 0.51 ms, full 1.05 ms).  Here:
+//   * LDS = a ring of RB node buffers (16 KiB: one node x 256 layers x 64 B) that streams
+//     continuously across tiles + a separate S/C region (4 x 16 KiB, [row r][layer z][64 B]);
+//   * 8 compute waves: phase A of tile k (StreamDec::phase_a, one barrier per section), the
+//     presolve S' = H_K^-1 S in registers (tables through scalar loads), then S'(k) into the S/C
+//     region once the region is free;
+//   * 4 loader waves issue every LDS-DMA (as in k_stream_syn) AND solve tile k-1 meanwhile: the
+//     round of iscore level y + 1 during section step y of tile k (term-parallel: one item per
+//     (target layer, section Y, node X) x 8 bytes, A_(Y,X) C(e_Y, z[Y:=X]) XORed into every C_r(z)
+//     with 64-bit LDS atomics; items grouped by (Y, X) so a wave's tables are uniform -> SGPRs);
+//   * after the last round the compute waves read C(k-1) into registers, hand the region over
+//     (S'(k) in) and store C(k-1): stores come from waves that never wait on vmcnt, so the
+//     loaders' counted DMA waits see loads only;
+//   * six workgroup barriers per tile (four section steps, rounds done, region free), all waves.
+// Tables and the per-level target lists live in global memory (L2 / scalar cache): the ring and
+// the S/C region take all 160 KiB of LDS.
+#pragma once
+
+#include "stream_decode.hpp"
+
+namespace clay {
+namespace bs {
+
+// PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
+// 2 = no output stores, 4 = no phase-A math, 8 = no presolve
+template <int KD, int G, int PROBE = 0>
+__global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(DecArgs a) {
+    using Kn = StreamDec<KD, G>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7u, wslot = blockIdx.x >> 3, ns = a.nslots;
+    const uint32_t sc = uint32_t(a.sc);
+    const typename Kn::Map tm(sc, a.region, ns, xcd, wslot);
+    const uint32_t ntile = tm.n;
+    if (ntile == 0) return;  // uniform per workgroup
+    const uint32_t RB = a.ring, NT = a.nt;
+    constexpr uint32_t BUF = uint32_t(Kn::BUF);
+    uint8_t *const scr = smem + RB * BUF;  // S/C region
+    const cu32p tabc = (cu32p)(a.tabs);  // constant address space: uniform loads become s_load
+
+    if (wave >= Kn::CWAVES) {
+        // ---------------- loader + solver waves ----------------
+        __builtin_amdgcn_s_setprio(3);
+        const int li = wave - Kn::CWAVES;
+        typename Kn::Loader L;
+        Kn::loader_init(L, sc, li, lane);
+        const uint32_t lds0 = lds_addr_of(smem);
+        const uint32_t nloads = ntile * NT;
+        uint32_t issued = 0;
+        auto issue_upto = [&](uint32_t lim) {
+            if (lim > nloads) lim = nloads;
+            for (; issued < lim; issued++) {
+                const uint32_t k = issued / NT, q = issued % NT;
+                Kn::issue(a, L, lds0 + (issued % RB) * BUF, a.node[a.load_node[q]], tm.tile(k, wslot, ns), li);
+            }
+        };
+        issue_upto(RB);
+        const uint8_t *zl = reinterpret_cast<const uint8_t *>(a.tabs) + kDecZList;
+        for (uint32_t k = 0; k <= ntile; k++) {
+            for (int y = 0; y < 4; y++) {
+                if (k < ntile) {
+                    // loads of step (k, y) landed; the loads issued after them may stay in flight
+                    const uint32_t qend = k * NT + a.sec_off[y + 1];
+                    wait_vm_rt(int((issued - qend) * uint32_t(Kn::BPL)));
+                }
+                lds_barrier();  // B_y(k): step (k, y) landed; C(k-1) of level y visible
+                if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
+                if (k == 0 || (PROBE & 1)) continue;
+                // ---- round of iscore level y + 1 of tile k - 1 ----
+                const uint32_t lv = uint32_t(y);
+                for (uint32_t gi = uint32_t(li); gi < 16u; gi += uint32_t(Kn::LOADERS)) {
+                    const uint32_t g0 = a.gstart[lv * 16u + gi], g1 = a.gstart[lv * 16u + gi + 1u];
+                    if (g0 == g1) continue;  // uniform
+                    const uint32_t Y = gi >> 2, X = gi & 3u;
+                    const uint32_t xe = uint32_t(__builtin_ctz(a.emask[Y]));
+                    const uint32_t ry = uint32_t(a.rix[4u * Y + xe]);
+                    const uint32_t sh = 2u * (3u - Y);
+                    GfTab t[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) t[r] = load_tab_c(tabc + (16u + (4u * Y + X) * 4u + uint32_t(r)) * 8u);
+                    const int32_t dz = (int32_t(X) - int32_t(xe)) * int32_t(1u << sh);  // z[Y := X] - z (z_Y = xe)
+                    const uint8_t *src = scr + ry * BUF;
+                    for (uint32_t it = g0 * 8u + uint32_t(lane); it < g1 * 8u; it += 64u) {
+                        const uint32_t z = zl[it >> 3], d8 = (it & 7u) * 8u;
+                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + uint32_t(int32_t(z) + dz) * 64u + d8);
+                        const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            if (uint32_t(r) < a.ne) {
+                                const uint64_t v = uint64_t(gf_mul_idx(i0, t[r])) | (uint64_t(gf_mul_idx(i1, t[r])) << 32);
+                                __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + z * 64u + d8), v,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        }
+                    }
+                }
+            }
+            lds_barrier();  // B_r(k): every atomic of tile k-1 done (lgkmcnt(0) before the barrier)
+            lds_barrier();  // B_w(k): the compute waves hold C(k-1); the region takes S'(k)
+        }
+        wait_vm0();
+        return;
+    }
+
+    // ---------------- compute waves ----------------
+    const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
+    const uint32_t emG = a.emask[G];
+    const int xeG = emG ? __builtin_ctz(emG) : -1;
+    for (uint32_t k = 0; k <= ntile; k++) {
+        uint32_t S[32];
+        if (k < ntile) {
+            const typename Kn::Tile t = tm.tile(k, wslot, ns);
+            const bool straddle = t.vend < t.b0 + uint32_t(Kn::W) && ((t.vend - t.b0) & 15u) == 8u;
+            const uint32_t pcs = (t.vend - t.b0) >> 4;
+            const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
+#pragma unroll
+            for (int w = 0; w < 32; w++) S[w] = 0;
+            Kn::template phase_a<(PROBE & 4) ? 2 : 0>(a, smem, k * NT, c0, poff0, xeG, S, RB);
+            // bit planes -> bytes, then S' = H_K^-1 S per slot (tables: scalar loads)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t v[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++) v[w] = S[j * 8 + w];
+                transpose8(v);
+#pragma unroll
+                for (int w = 0; w < 8; w++) S[j * 8 + w] = v[w];
+            }
+            if constexpr (!(PROBE & 8)) {
+                sfor<4>([&](auto gc) BS_INL {
+                    constexpr int g = decltype(gc)::value;
+                    uint32_t U[4][2] = {};
+                    sfor<4>([&](auto jc) BS_INL {
+                        constexpr int j = decltype(jc)::value;
+                        const GfIdx i0 = gf_idx(S[j * 8 + 2 * g]), i1 = gf_idx(S[j * 8 + 2 * g + 1]);
+                        // an opaque base per (g, j): the 4 tables are loaded here, not all 16 hoisted
+                        // out of the tile loop into SGPRs (which spilled into VGPR lanes)
+                        uint32_t zoff = 0;
+                        asm volatile("" : "+s"(zoff));
+                        const cu32p tj = tabc + zoff;
+                        sfor<4>([&](auto rc) BS_INL {
+                            constexpr int r = decltype(rc)::value;
+                            const GfTab tb = load_tab_c(tj + (r * 4 + j) * 8);
+                            U[r][0] ^= gf_mul_idx(i0, tb);
+                            U[r][1] ^= gf_mul_idx(i1, tb);
+                        });
+                    });
+                    sfor<4>([&](auto rc) BS_INL {
+                        constexpr int r = decltype(rc)::value;
+                        S[r * 8 + 2 * g] = U[r][0];
+                        S[r * 8 + 2 * g + 1] = U[r][1];
+                    });
+                });
+            }
+        } else {
+#pragma unroll
+            for (int y = 0; y < 4; y++) lds_barrier();  // B_y(ntile): the last tile's rounds
+        }
+        lds_barrier();  // B_r(k): C(k-1) complete in the region
+        // C(k-1) -> registers: 1,024 rows x 64 B, lane = one 16-byte piece of 16 rows per pass
+        uint4 ov[8];
+        if (k >= 1) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) ov[i] = *reinterpret_cast<const uint4 *>(scr + (uint32_t(i) * 512u + threadIdx.x) * 16u);
+        }
+        lds_barrier();  // B_w(k): the region is free
+        if (k < ntile) {
+            const uint32_t z0 = Kn::layer0(opq(c0));
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p) =
+                        make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
+        }
+        if (k >= 1 && !(PROBE & 2)) {
+            // piece i of this lane: row r = i / 2 (compile time), layer 128 (i & 1) + tid / 4,
+            // 16 bytes at 16 (tid & 3)
+            const typename Kn::Tile t = tm.tile(k - 1, wslot, ns);
+            const uint32_t pc = (threadIdx.x & 3u) * 16u, zl0 = threadIdx.x >> 2;
+            const bool full = t.b0 + pc + 16u <= t.vend, half = !full && t.b0 + pc + 8u <= t.vend;
+            const uint64_t off0 = uint64_t(zl0) * sc + t.b0 + pc;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int r = i >> 1;
+                uint8_t *dst = a.out[r];
+                if (uint32_t(r) >= a.ne || !dst) continue;
+                uint8_t *o = dst + off0 + uint64_t(i & 1) * 128u * sc;
+                if (full) *reinterpret_cast<uint4 *>(o) = ov[i];
+                else if (half) *reinterpret_cast<uint2 *>(o) = make_uint2(ov[i].x, ov[i].y);
+            }
+        }
+    }
+}
+
+}  // namespace bs
+}  // namespace clay

@@ -127,3 +127,68 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, auto_exe
     clay_amd.set_exec_mode("stream")
     for e in er:
         assert np.array_equal(a[e], b[e]), e
+
+
+def fused2_eligible(c, er):
+    """k_stream_fused2: at most one erasure per y-section and a ring of 6 node buffers that holds
+    any two neighbouring sections' surviving real nodes."""
+    if not stream_eligible(c, er):
+        return False
+    alive = [0] * c.t
+    for i in range(c.n):
+        if i not in er:
+            alive[_internal(c, i) // c.q] += 1
+    return all(alive[y] + (alive[y + 1] if y + 1 < c.t else 0) <= 6 for y in range(c.t))
+
+
+@pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
+@pytest.mark.parametrize("sc", [512, 520, 64 * 37 + 40])
+def test_fused2_decode_random_inputs(oracle_mod, torch_cuda, cfg, sc):
+    """Exec mode "stream-fused2" (stream_fused2.hpp): every eligible pattern of up to 4 erasures on
+    random chunks, erased data chunks bit-exact vs the oracle; the other patterns fall back."""
+    torch = torch_cuda
+    c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc + 3 * cfg[0])
+    pats = [list(e) for r in (2, 3, 4) for e in itertools.combinations(range(c.n), r)
+            if fused2_eligible(c, list(e))]
+    pats = [pats[i] for i in rng.permutation(len(pats))[:40]]
+    pats.insert(0, [0, 4, 8, 12] if cfg == (10, 4, 13) else [0, 4, 8, 11])
+    prev = clay_amd.set_exec_mode("stream-fused2")
+    try:
+        for er in pats:
+            chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+            got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
+            assert clay_amd.last_exec_path() == "stream-fused2", (er, clay_amd.last_exec_path())
+            ref = _oracle_erased(o, c, chunks, er)
+            for e in er:
+                if e < c.k:
+                    assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e)
+    finally:
+        clay_amd.set_exec_mode(prev)
+
+
+@pytest.mark.parametrize("sc", [520, 64 * 8 * 33 + 24])
+def test_fused2_decode_codeword_incl_parity_and_grouped(oracle_mod, torch_cuda, sc):
+    """The BASELINE worst case {0,4,8,12} on a codeword (every rebuilt chunk incl. parity node 12)
+    and on random inputs against the grouped plan executor (parity outputs included)."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    chunk = c.sub_chunk_no * sc
+    er = [0, 4, 8, 12]
+    ref = o.encode_array(np.random.default_rng(sc).integers(0, 256, c.k * chunk, dtype=np.uint8))
+    prev = clay_amd.set_exec_mode("stream-fused2")
+    try:
+        got = _decode_dev(torch, c, ref, er, chunk)
+        assert clay_amd.last_exec_path() == "stream-fused2"
+        for e in er:
+            assert np.array_equal(got[e], ref[e]), e
+        chunks = np.random.default_rng(sc + 1).integers(0, 256, (c.n, chunk), dtype=np.uint8)
+        a = _decode_dev(torch, c, chunks, er, chunk)
+        clay_amd.set_exec_mode("grouped")
+        b = _decode_dev(torch, c, chunks, er, chunk)
+        assert clay_amd.last_exec_path() == "grouped"
+        for e in er:
+            assert np.array_equal(a[e], b[e]), e
+    finally:
+        clay_amd.set_exec_mode(prev)
