@@ -38,6 +38,7 @@
 #include "kernels.hpp"
 #include "plan.hpp"
 #include "tuning.hpp"
+#include "encode3_args.hpp"
 
 namespace clay {
 
@@ -1431,6 +1432,38 @@ static Error launch_stream(CodeState &cs, const DevProps &prop, const uint8_t *c
     return Error{};
 }
 
+hipError_t launch_stream_encode3_kernel(int loaders, const bs::Enc3Args &a, hipStream_t stream, int dev);  // encode_stream3.hip
+
+// The streaming encode for (9,3,11) (stream_encode3.hpp): any sub-chunk size >= 16 and any row
+// alignment (LDS-DMA reads, unaligned 16-byte stores, byte-exact partial tiles).
+static Error launch_stream3(CodeState &cs, const DevProps &prop, const uint8_t *const *data, uint8_t *const *par,
+                            size_t n_stripes, size_t sc, hipStream_t stream, int loaders, bool *done) {
+    using S = bs::Shape<9, 3>;
+    const clay_code_t &c = cs.code;
+    if (c.k != 9 || c.m != 3 || c.d != 11 || sc < 16 || double(S::ALPHA) * double(sc) >= 4294967296.0) return Error{};
+    for (int p = 0; p < 3; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    const uint32_t W = 512;
+    bs::Enc3Args a{};
+    a.sc = sc;
+    a.ntiles = uint32_t((sc + W - 1) / W);
+    a.per_xcd = (a.ntiles + 7) / 8;
+    a.ns = std::min(uint32_t(std::max(1, prop.cus / 8)), a.per_xcd);
+    for (size_t s = 0; s < n_stripes; s++) {
+        for (int i = 0; i < 9; i++) a.data[i] = data[s * 9 + i];
+        for (int x = 0; x < 3; x++) a.par[x] = par[s * 3 + x];
+        CLAY_HIP(launch_stream_encode3_kernel(loaders, a, stream, prop.dev));
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "stream3-k9m3-w512-l%d", loaders == 7 ? 7 : 2);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
 static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data, uint8_t *const *par,
                               size_t n_stripes, size_t chunk, hipStream_t stream, int mode, int tile, bool *done) {
     *done = false;
@@ -1450,6 +1483,11 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     Error e;
     const int key = int(c.k * 100 + c.m);
     // streaming kernel (q = 4, t = 4, k 9 / 10): auto's first choice; tile = loader waves
+    // (9,3) streaming kernel: any row alignment; tile = loader waves (2, or 7)
+    if (key == 903 && (mode == kModeStream || mode == kModeAuto)) {
+        e = launch_stream3(cs, prop, data, par, n_stripes, sc, stream, tile == 7 ? 7 : 2, done);
+        if (e || *done || mode == kModeStream) return e;
+    }
     if (rows8 && (mode == kModeStream || mode == kModeAuto)) {
         if (key == 1004 || key == 904) {
             const int l = tile ? tile : 4;
@@ -2393,7 +2431,7 @@ int clay_set_encode_path(int mode) {
     case kModeAuto: case kModeStaged: case kModeFused: ok = tile == 0; break;
     case kModeBs: ok = tile == 0 || tile == 1 || tile == 4; break;     // v1 lanes of 32 B per column group
     case kModeBs6: ok = tile == 0 || tile == 4; break;                // 256- / 128-byte tiles
-    case kModeStream: ok = tile == 0 || tile == 1 || tile == 2 || tile == 4; break;  // loader waves
+    case kModeStream: ok = tile == 0 || tile == 1 || tile == 2 || tile == 4 || tile == 7; break;  // loader waves
     default: ok = false;
     }
     if (!ok) return -1;

@@ -76,6 +76,29 @@ def test_bitsliced_encode_matches_oracle(oracle_mod, cfg, tile, scale):
     assert np.array_equal(got, ref), (cfg, tile, scale)
 
 
+STREAM3_SC = [16, 17, 100, 511, 512, 513, 1000, 4098, 512 * 256 + 37, 512 * 300 * 8 + 2, 3_314_018 // 64]
+
+
+@pytest.mark.parametrize("loaders", [2, 7])
+@pytest.mark.parametrize("sc", STREAM3_SC)
+def test_stream3_encode_matches_oracle(oracle_mod, loaders, sc):
+    """(9,3,11) streaming kernel (stream_encode3.hpp): any sub-chunk size >= 16 (odd sizes, one
+    partial tile, 2 mod 8 rows like the 256 MiB BASELINE chunk, more tiles than workgroups),
+    2 / 7 loader waves, bit-exact against the oracle."""
+    c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
+    n = 9 * c.sub_chunk_no * sc - 5
+    data = rand_bytes(sc * 3 + loaders, n)
+    ref = o.encode_array(data)
+    assert ref.shape[1] == c.sub_chunk_no * sc
+    set_encode_path("stream", loaders)
+    try:
+        got = c.encode_array(data)
+        assert last_encode_path().startswith("stream3"), last_encode_path()
+    finally:
+        set_encode_path("auto", 0)
+    assert np.array_equal(got, ref), (sc, loaders)
+
+
 STREAM_SC = [16, 24, 64, 72, 104, 128, 256, 1064, 6440, 8 * 256 * 32, 8 * 256 * 32 + 8, 64 * 300 + 40,
              64 * 2000 + 8, 8 * 256 * 32 * 3 + 4096 + 24]
 
