@@ -19,8 +19,7 @@ static float run(RepStreamArgs sa, int reps) {
     using Kn = BsRepairStream<9, 3, 0, PARTS, LOADERS>;
     auto fn = &k_bs_repair_stream<9, 3, 0, PARTS, LOADERS, PROBE>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
-    sa.ntiles = uint32_t((sa.r.sc + Kn::W - 1) / Kn::W);
-    sa.per_xcd = (sa.ntiles + 7) / 8;
+    sa.region = uint32_t(((sa.r.sc + 7) / 8 + 31) / 32 * 32);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);

@@ -10,8 +10,7 @@ struct Enc3Args {
     const uint8_t *data[9];
     uint8_t *par[3];
     uint64_t sc;
-    uint32_t ntiles;   // tiles of W bytes (the last one partial if W does not divide sc)
-    uint32_t per_xcd;  // tiles per XCD region
+    uint32_t region;   // XCD region bytes (StreamMap: full tiles round robin, the remainder split)
     uint32_t ns;       // workgroups per XCD
 };
 

@@ -1448,9 +1448,8 @@ static Error launch_stream3(CodeState &cs, const DevProps &prop, const uint8_t *
     const uint32_t W = 512;
     bs::Enc3Args a{};
     a.sc = sc;
-    a.ntiles = uint32_t((sc + W - 1) / W);
-    a.per_xcd = (a.ntiles + 7) / 8;
-    a.ns = std::min(uint32_t(std::max(1, prop.cus / 8)), a.per_xcd);
+    a.region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
+    a.ns = std::min(uint32_t(std::max(1, prop.cus / 8)), std::max(1u, (a.region + W - 1) / W));
     for (size_t s = 0; s < n_stripes; s++) {
         for (int i = 0; i < 9; i++) a.data[i] = data[s * 9 + i];
         for (int x = 0; x < 3; x++) a.par[x] = par[s * 3 + x];
@@ -1886,8 +1885,10 @@ static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const 
     a.sec_off[4] = nt;
     a.nt = nt;
     if (nt == 0) return Error{};
+    // the split / local kernels stream through R - 1 buffers (the last holds tables): a step's
+    // loads are issued during the step before it, across tiles too (section 3 -> section 0)
     for (int y = 0; y < 4; y++)
-        if (n[y] > R || (y < 3 && n[y] + n[y + 1] > R)) return Error{};
+        if (n[y] > R - 1 || n[y] + n[(y + 1) % 4] > R - 1) return Error{};
     if (R < 5) return Error{};  // S/C region (4 buffers) + the phase-B table buffer
     a.ring = R;
     a.sc = sc;
@@ -2057,9 +2058,11 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
     if (e || !ok) return e;
     constexpr uint32_t RB = 6;
+    // the loads of a step are issued during the step before it (the ring holds both), also
+    // across tiles: section 3 of tile k and section 0 of tile k + 1
     for (int y = 0; y < 4; y++) {
         const uint32_t ny = a.sec_off[y + 1] - a.sec_off[y];
-        const uint32_t nn = y < 3 ? a.sec_off[y + 2] - a.sec_off[y + 1] : 0u;
+        const uint32_t nn = y < 3 ? a.sec_off[y + 2] - a.sec_off[y + 1] : a.sec_off[1] - a.sec_off[0];
         if (ny > RB || ny + nn > RB) return Error{};
     }
     a.ring = RB;

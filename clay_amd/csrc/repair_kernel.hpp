@@ -272,8 +272,7 @@ struct BsRepair {
 // ---------------------------------------------------------------------------------------------
 struct RepStreamArgs {
     RepArgs r;
-    uint32_t ntiles;   // tiles of W bytes (the last one partial if W does not divide sc)
-    uint32_t per_xcd;  // tiles per XCD region
+    uint32_t region;   // XCD region bytes (StreamMap: full tiles round robin, the remainder split)
     uint32_t ns;       // workgroups per XCD
 };
 
@@ -403,8 +402,8 @@ struct BsRepairStream {
     }
 };
 
-// grid = 8 * ns workgroups (one per CU); XCD x owns full tiles [x * per_xcd, (x + 1) * per_xcd),
-// its ns workgroups take them round robin.
+// grid = 8 * ns workgroups (one per CU); XCD x owns bytes [x * region, (x + 1) * region): full
+// tiles round robin over its ns workgroups, the remainder one partial tile each (StreamMap).
 // PROBE (bench_tools/repair_probe only; the library instantiates 0): bit 1 = compute waves skip
 // the math (garbage outputs), 2 = loaders issue no DMA, 4 = no output stores.
 template <int KD, int M, int Y0, int PARTS, int LOADERS, int PROBE = 0>
@@ -417,14 +416,11 @@ __global__ __launch_bounds__((BsRepairStream<KD, M, Y0, PARTS, LOADERS>::BLOCK))
     const RepArgs &a = sa.r;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, ns = sa.ns;
-    const uint32_t t0 = xcd * sa.per_xcd;
-    const uint32_t t1 = t0 + sa.per_xcd < sa.ntiles ? t0 + sa.per_xcd : sa.ntiles;
-    const uint32_t ntile = t0 + slot < t1 ? (t1 - t0 - slot + ns - 1) / ns : 0u;
+    const uint32_t sc32 = uint32_t(a.sc);
+    const StreamMap tm(sc32, sa.region, ns, xcd, slot, uint32_t(Kn::W));
+    const uint32_t ntile = uint32_t(tm.ntile());
     const uint32_t x0 = a.x0;
     if (ntile == 0) return;  // uniform per workgroup
-    const uint32_t sc32 = uint32_t(a.sc);
-    auto tile_b0 = [&](uint32_t k) { return (t0 + slot + k * ns) * uint32_t(Kn::W); };
-    auto tile_end = [&](uint32_t b0) { return b0 + uint32_t(Kn::W) < sc32 ? b0 + uint32_t(Kn::W) : sc32; };
     const uint32_t nsteps = ntile * uint32_t(T);
 
     if (wave >= Kn::CWAVES) {
@@ -441,8 +437,8 @@ __global__ __launch_bounds__((BsRepairStream<KD, M, Y0, PARTS, LOADERS>::BLOCK))
             for (; issued < lim; issued++) {
                 const uint32_t k = issued / uint32_t(NT), q = issued % uint32_t(NT);
                 const int nd = Kn::node_of(int(q), x0);
-                const uint32_t b0 = tile_b0(k);
-                if constexpr (!(PROBE & 2)) Kn::issue(a, L, lds0 + (issued % NB) * NODE, a.h[nd], b0, tile_end(b0), li);
+                const StreamTile t = tm.tile(int(k), slot, ns);
+                if constexpr (!(PROBE & 2)) Kn::issue(a, L, lds0 + (issued % NB) * NODE, a.h[nd], t.b0, t.vend, li);
             }
         };
         issue_upto(NB);
@@ -450,7 +446,8 @@ __global__ __launch_bounds__((BsRepairStream<KD, M, Y0, PARTS, LOADERS>::BLOCK))
             const uint32_t k = s / uint32_t(T), st = s % uint32_t(T);
             // loads of step s landed (everything issued after them may stay in flight)
             const uint32_t qend = k * uint32_t(NT) + uint32_t(st + 1 < uint32_t(T) ? Kn::soff(int(st) + 1) : NT);
-            const uint32_t b0 = tile_b0(k), vend = tile_end(b0);
+            const StreamTile t = tm.tile(int(k), slot, ns);
+            const uint32_t b0 = t.b0, vend = t.vend;
             if (vend < b0 + uint32_t(Kn::W)) {
                 // partial tile: everything landed, then the straddling pieces of this step
                 wait_vm0();
@@ -478,7 +475,8 @@ __global__ __launch_bounds__((BsRepairStream<KD, M, Y0, PARTS, LOADERS>::BLOCK))
     const uint32_t jr = active ? j : 0u;  // idle lanes of the last wave compute row 0, store nothing
     uint32_t acc[Q * 8];
     for (uint32_t k = 0; k < ntile; k++) {
-        const uint32_t b0 = tile_b0(k), vend = tile_end(b0);
+        const StreamTile t = tm.tile(int(k), slot, ns);
+        const uint32_t b0 = t.b0, vend = t.vend;
 #pragma unroll
         for (int w = 0; w < Q * 8; w++) acc[w] = 0;
         sfor<T>([&](auto sc_) BS_INL {

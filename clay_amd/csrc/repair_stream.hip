@@ -43,8 +43,7 @@ static hipError_t launch_stream(const bs::RepArgs &a, hipStream_t stream, int de
     }
     bs::RepStreamArgs sa{};
     sa.r = a;
-    sa.ntiles = uint32_t((a.sc + Kn::W - 1) / Kn::W);
-    sa.per_xcd = (sa.ntiles + 7) / 8;
+    sa.region = uint32_t(((a.sc + 7) / 8 + 31) / 32 * 32);
     sa.ns = ns;
     bs::k_bs_repair_stream<KD, M, Y0, PARTS, LOADERS><<<dim3(ns * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(sa);
     const hipError_t e = hipGetLastError();

@@ -53,16 +53,18 @@ struct StreamTile {
     uint32_t b0, vend;  // positions [b0, b0 + 256) of every row, valid below vend
 };
 
-// XCD x owns bytes [x * region, min((x + 1) * region, sc)); full tiles round robin over
-// the XCD's ns workgroups, the remainder one partial tile per workgroup (its last).
+// XCD x owns bytes [x * region, min((x + 1) * region, sc)); full W-byte tiles round robin over
+// the XCD's ns workgroups, the remainder one partial tile per workgroup (its last), so every
+// workgroup of an XCD streams the same number of bytes to within 32.
 struct StreamMap {
-    uint32_t x0, x1, nfull, p0, p1;
-    __device__ StreamMap(uint32_t sc, uint32_t region, uint32_t ns, uint32_t xcd, uint32_t slot) {
+    uint32_t x0, x1, nfull, p0, p1, w;
+    __device__ StreamMap(uint32_t sc, uint32_t region, uint32_t ns, uint32_t xcd, uint32_t slot, uint32_t W = 256u) {
+        w = W;
         x0 = xcd * region;
         x1 = x0 + region < sc ? x0 + region : sc;
         nfull = p0 = p1 = 0;
         if (x0 >= x1) return;
-        const uint32_t len = x1 - x0, round = ns * 256u;
+        const uint32_t len = x1 - x0, round = ns * W;
         nfull = len / round;
         const uint32_t left = len - nfull * round;
         const uint32_t wp = ((left + ns - 1) / ns + 31u) & ~31u;
@@ -75,8 +77,8 @@ struct StreamMap {
     __device__ int ntile() const { return int(nfull) + (p0 < p1 ? 1 : 0); }
     __device__ StreamTile tile(int k, uint32_t slot, uint32_t ns) const {
         if (uint32_t(k) < nfull) {
-            const uint32_t b0 = x0 + (uint32_t(k) * ns + slot) * 256u;
-            return {b0, b0 + 256u};
+            const uint32_t b0 = x0 + (uint32_t(k) * ns + slot) * w;
+            return {b0, b0 + w};
         }
         return {p0, p1};
     }

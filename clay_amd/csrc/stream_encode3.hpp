@@ -220,8 +220,8 @@ struct StreamEnc3 {
     }
 };
 
-// grid = 8 * ns (one workgroup per CU); XCD x owns tiles [x * per_xcd, (x + 1) * per_xcd), its ns
-// workgroups take them round robin.  PROBE (bench_tools only): 1 = no math, 2 = no DMA, 4 = no stores.
+// grid = 8 * ns (one workgroup per CU); XCD x owns bytes [x * region, (x + 1) * region): full
+// tiles round robin over its ns workgroups, the remainder one partial tile each (StreamMap).  PROBE (bench_tools only): 1 = no math, 2 = no DMA, 4 = no stores.
 template <int KD, int M, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc3<KD, M, LOADERS>::BLOCK)) void k_stream_encode3(Enc3Args a) {
     using Kn = StreamEnc3<KD, M, LOADERS>;
@@ -230,13 +230,10 @@ __global__ __launch_bounds__((StreamEnc3<KD, M, LOADERS>::BLOCK)) void k_stream_
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, ns = a.ns;
-    const uint32_t t0 = xcd * a.per_xcd;
-    const uint32_t t1 = t0 + a.per_xcd < a.ntiles ? t0 + a.per_xcd : a.ntiles;
-    const uint32_t ntile = t0 + slot < t1 ? (t1 - t0 - slot + ns - 1) / ns : 0u;
-    if (ntile == 0) return;  // uniform per workgroup
     const uint32_t sc32 = uint32_t(a.sc);
-    auto tile_b0 = [&](uint32_t k) { return (t0 + slot + k * ns) * uint32_t(Kn::W); };
-    auto tile_end = [&](uint32_t b0) { return b0 + uint32_t(Kn::W) < sc32 ? b0 + uint32_t(Kn::W) : sc32; };
+    const StreamMap tm(sc32, a.region, ns, xcd, slot, uint32_t(Kn::W));
+    const uint32_t ntile = uint32_t(tm.ntile());
+    if (ntile == 0) return;  // uniform per workgroup
     const uint32_t nsteps = ntile * uint32_t(STEPS);
 
     if (wave >= Kn::CWAVES) {
@@ -256,15 +253,16 @@ __global__ __launch_bounds__((StreamEnc3<KD, M, LOADERS>::BLOCK)) void k_stream_
             if (lim > nloads) lim = nloads;
             for (; issued < lim; issued++) {
                 const uint32_t k = issued / uint32_t(NT), q = issued % uint32_t(NT);
-                const uint32_t b0 = tile_b0(k);
-                if constexpr (!(PROBE & 2)) Kn::issue(L, lds0 + (issued % NB) * NODE, nbase_of(q), b0, tile_end(b0), li);
+                const StreamTile t = tm.tile(int(k), slot, ns);
+                if constexpr (!(PROBE & 2)) Kn::issue(L, lds0 + (issued % NB) * NODE, nbase_of(q), t.b0, t.vend, li);
             }
         };
         issue_upto(NB);
         for (uint32_t s = 0; s < nsteps; s++) {
             const uint32_t k = s / uint32_t(STEPS), st = s % uint32_t(STEPS);
             const uint32_t qs = k * uint32_t(NT) + st * uint32_t(Q), qend = qs + uint32_t(Q);
-            const uint32_t b0 = tile_b0(k), vend = tile_end(b0);
+            const StreamTile t = tm.tile(int(k), slot, ns);
+            const uint32_t b0 = t.b0, vend = t.vend;
             if (vend < b0 + uint32_t(Kn::W)) {
                 wait_vm0();  // partial tile: everything landed, then this step's straddling pieces
                 if constexpr (!(PROBE & 2))
@@ -290,7 +288,8 @@ __global__ __launch_bounds__((StreamEnc3<KD, M, LOADERS>::BLOCK)) void k_stream_
     uint32_t H[2][8];  // U values later PFT pairs need (see the group ends)
     for (uint32_t s = 0; s < nsteps; s++) {
         const uint32_t k = s / uint32_t(STEPS), st = s % uint32_t(STEPS), G = st / 3u, Y = st % 3u;
-        const uint32_t b0 = tile_b0(k), vend = tile_end(b0);
+        const StreamTile t = tm.tile(int(k), slot, ns);
+        const uint32_t b0 = t.b0, vend = t.vend;
         lds_barrier();  // step s landed
         const uint32_t gq0 = k * uint32_t(NT) + st * uint32_t(Q);
         uint32_t co = c;

@@ -243,7 +243,8 @@ size_t clay_workspace_bytes(int device);
 
 /* Encode path selection (process-wide; tests and benchmarks).  Low byte = path:
  *   0 auto      -- the streaming kernel for q = 4, t = 4 codes with k = 9 / 10 (the
- *                  BASELINE (10,4,13)); else the bit-sliced v1 kernel if the code has a
+ *                  BASELINE (10,4,13)) and for (9,3,11) (k_stream_encode3: any sub-chunk
+ *                  size >= 16 and any alignment); else the bit-sliced v1 kernel if the code has a
  *                  compiled instantiation; else the byte-sliced fused kernel when the
  *                  parity is one y-section; else the staged plan executor.  Batches of
  *                  >= 4 stripes of <= 4 MiB of data run as one staged launch per level.
@@ -258,7 +259,8 @@ size_t clay_workspace_bytes(int device);
  *                  tiles, 4 = 128-B tiles
  *   5 stream    -- the streaming kernel (stream_encode.hpp); variant = loader waves
  *                  for (10,4,13): 0 (= 4, the default), 1, 2, 4; (9,4,12) always runs
- *                  4 loader waves (its variant is accepted and ignored)
+ *                  4 loader waves (its variant is accepted and ignored); (9,3,11): 7 loader
+ *                  waves for variant 7, else 2 (stream_encode3.hpp)
  * Bits 8..15 = variant.  Every accepted (path, variant) produces the reference's
  * parity bytes; any other value returns -1 and leaves the setting unchanged.
  * Returns the previous setting (path | variant << 8). */
@@ -285,6 +287,9 @@ int clay_set_encode_path(int mode);
  *                streaming decode ("stream-split"); everything else as auto
  *   4 stream-fused -- as stream, but on the fused single-launch k_stream_decode ("stream")
  *   5 stream-local -- every decode the local kernel takes on it ("stream-local"); else as auto
+ *   6 stream-fused2 -- decodes with one erasure per y-section on the fused decode v2
+ *                (k_stream_fused2, "stream-fused2"; ring of 6 buffers: needs any two
+ *                neighbouring sections to hold <= 6 surviving real nodes); else as auto
  * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
  * (planner and executor tuning) are read once when the library is loaded.
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
@@ -292,7 +297,7 @@ int clay_set_encode_path(int mode);
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
  * "tile" (k_texec), "grouped" (k_gexec), "stream-split" (k_stream_syn + k_stream_solve),
- * "stream" (k_stream_decode), "stream-local" (k_stream_local), "bs-repair-stream" (k_bs_repair_stream), "bs-repair"
+ * "stream" (k_stream_decode), "stream-local" (k_stream_local), "stream-fused2" (k_stream_fused2), "bs-repair-stream" (k_bs_repair_stream), "bs-repair"
  * (k_bs_repair) or "none". */
 const char *clay_last_exec_path(void);
 

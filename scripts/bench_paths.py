@@ -80,7 +80,16 @@ def encode_batch_cfg(k, m, d, stripe, n):
            {"input_GiBps": round(n * k * chunk / (ms * 1e-3) / 2**30, 1)})
 
 
-def decode_cfg(k, m, d, stripe, er):
+def decode_cfg(k, m, d, stripe, er, mode=None):
+    prev = clay_amd.set_exec_mode(mode) if mode else None
+    try:
+        _decode_cfg(k, m, d, stripe, er)
+    finally:
+        if prev:
+            clay_amd.set_exec_mode(prev)
+
+
+def _decode_cfg(k, m, d, stripe, er):
     c = ClayCode(k, m, d)
     chunk = c.encoded_chunk_size(stripe)
     full = rnd(c.n, chunk, 2)
@@ -135,6 +144,8 @@ if __name__ == "__main__":
             ("batch", lambda: encode_batch_cfg(4, 2, 5, 1 << 20, 256)),
             ("decode", lambda: decode_cfg(4, 2, 5, 64 << 20, [0])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
+            ("split", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "stream")),
+            ("split", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "stream-fused2")),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0])),
             ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
             ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),

@@ -138,7 +138,7 @@ def fused2_eligible(c, er):
     for i in range(c.n):
         if i not in er:
             alive[_internal(c, i) // c.q] += 1
-    return all(alive[y] + (alive[y + 1] if y + 1 < c.t else 0) <= 6 for y in range(c.t))
+    return all(alive[y] + alive[(y + 1) % c.t] <= 6 for y in range(c.t))  # incl. section 3 -> next tile's 0
 
 
 @pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
