@@ -108,7 +108,7 @@ template <int KD, int PROBE = 0>
 static hipError_t launch_f2(const bs::DecArgs &a, hipStream_t stream, int dev) {
     static std::mutex mu;
     static std::set<int> done;
-    const int lds = int(a.ring + 4) * bs::kDecBuf;  // ring + S/C region
+    const int lds = int(a.ring + a.ne) * bs::kDecBuf;  // ring + S/C region (ne rows)
     {
         std::lock_guard<std::mutex> lk(mu);
         if (!done.count(dev)) {

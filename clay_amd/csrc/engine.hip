@@ -2047,7 +2047,7 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
 hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
 
 // Fused decode v2 (stream_fused2.hpp): one erasure per y-section, one launch, rounds of tile k-1
-// on the loader waves while tile k streams.  Ring of 6 node buffers + the S/C region.
+// on the loader waves while tile k streams.  Ring of 10 - ne node buffers + the S/C region.
 template <int KD>
 static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
                                   const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream, bool *done) {
@@ -2057,7 +2057,7 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     bool ok = false;
     Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
     if (e || !ok) return e;
-    constexpr uint32_t RB = 6;
+    const uint32_t RB = 10 - a.ne;  // the S/C region takes ne of the 10 node buffers of LDS
     // the loads of a step are issued during the step before it (the ring holds both), also
     // across tiles: section 3 of tile k and section 0 of tile k + 1
     for (int y = 0; y < 4; y++) {

@@ -6,8 +6,8 @@
 // Why not k_stream_decode (the fused kernel of stream_decode.hpp)?  There the compute waves run
 // phase B themselves and its S/C region aliases ring buffers, so every tile drains the load
 // pipeline (measured: memory + phase A 0.51 ms, full 1.05 ms).  Here:
-//   * LDS = a ring of RB node buffers (16 KiB: one node x 256 layers x 64 B) that streams
-//     continuously across tiles + a separate S/C region (4 x 16 KiB, [row r][layer z][64 B]);
+//   * LDS = a ring of RB = 10 - ne node buffers (16 KiB: one node x 256 layers x 64 B) that
+//     streams continuously across tiles + a separate S/C region (ne x 16 KiB, [row r][z][64 B]);
 //   * 8 compute waves: phase A of tile k (StreamDec::phase_a, one barrier per section), the
 //     presolve S' = H_K^-1 S in registers (tables through scalar loads), then S'(k) into the S/C
 //     region once the region is free;
@@ -168,17 +168,20 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         uint4 ov[8];
         if (k >= 1) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) ov[i] = *reinterpret_cast<const uint4 *>(scr + (uint32_t(i) * 512u + threadIdx.x) * 16u);
+            for (int i = 0; i < 8; i++)
+                if (uint32_t(i >> 1) < a.ne)  // rows of the region: ne (it holds ne x 16 KiB)
+                    ov[i] = *reinterpret_cast<const uint4 *>(scr + (uint32_t(i) * 512u + threadIdx.x) * 16u);
         }
         lds_barrier();  // B_w(k): the region is free
         if (k < ntile) {
             const uint32_t z0 = Kn::layer0(opq(c0));
 #pragma unroll
             for (int r = 0; r < 4; r++)
+                if (uint32_t(r) < a.ne)
 #pragma unroll
-                for (int g = 0; g < 4; g++)
-                    *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p) =
-                        make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
+                    for (int g = 0; g < 4; g++)
+                        *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p) =
+                            make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
         }
         if (k >= 1 && !(PROBE & 2)) {
             // piece i of this lane: row r = i / 2 (compile time), layer 128 (i & 1) + tid / 4,

@@ -130,15 +130,16 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, auto_exe
 
 
 def fused2_eligible(c, er):
-    """k_stream_fused2: at most one erasure per y-section and a ring of 6 node buffers that holds
-    any two neighbouring sections' surviving real nodes."""
+    """k_stream_fused2: at most one erasure per y-section and a ring of 10 - e node buffers that
+    holds any two neighbouring sections' surviving real nodes."""
     if not stream_eligible(c, er):
         return False
     alive = [0] * c.t
     for i in range(c.n):
         if i not in er:
             alive[_internal(c, i) // c.q] += 1
-    return all(alive[y] + alive[(y + 1) % c.t] <= 6 for y in range(c.t))  # incl. section 3 -> next tile's 0
+    rb = 10 - len(er)
+    return all(alive[y] + alive[(y + 1) % c.t] <= rb for y in range(c.t))  # incl. section 3 -> next tile's 0
 
 
 @pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
