@@ -770,16 +770,19 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_syn(DecArg
                 const GfIdx i0 = gf_idx(S[j * 8 + 2 * g]), i1 = gf_idx(S[j * 8 + 2 * g + 1]);
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    const GfTab tb = Kn::tab_at(tl, r * 4 + j);
-                    U[r][0] ^= gf_mul_idx(i0, tb);
-                    U[r][1] ^= gf_mul_idx(i1, tb);
+                    if (uint32_t(r) < a.ne) {  // the erased rows only (uniform)
+                        const GfTab tb = Kn::tab_at(tl, r * 4 + j);
+                        U[r][0] ^= gf_mul_idx(i0, tb);
+                        U[r][1] ^= gf_mul_idx(i1, tb);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                *reinterpret_cast<uint2 *>(wtile + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) =
-                    make_uint2(U[r][0], U[r][1]);
+                if (uint32_t(r) < a.ne)  // S' rows of the erased nodes only: ne x 16 KiB of the tile's 64 KiB
+                    *reinterpret_cast<uint2 *>(wtile + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u) =
+                        make_uint2(U[r][0], U[r][1]);
         }
     }
 }
@@ -823,7 +826,8 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
     };
     auto tile_b0 = [&](uint32_t k) { return (t0 + wslot + k * ns) * SW; };
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++) dma_check(tile_b0(0), j);
+    for (uint32_t j = 0; j < 4; j++)
+        if (j < a.ne) dma_check(tile_b0(0), j);  // S' rows of the erased nodes only
     // output stores of a full tile per lane (issued after the next tile's DMA, so the wait for
     // that DMA lets them stay in flight): 2 per erased index with an output
     uint32_t nstores = 0;
@@ -854,7 +858,8 @@ __global__ __launch_bounds__(1024) void k_stream_solve(DecArgs a) {
         lds_barrier();  // the region is free
         if (k + 1 < ntile)
 #pragma unroll
-            for (uint32_t j = 0; j < 4; j++) dma_check(tile_b0(k + 1), j);
+            for (uint32_t j = 0; j < 4; j++)
+                if (j < a.ne) dma_check(tile_b0(k + 1), j);
         if constexpr (!(PROBE & 2)) {
             const bool full = b0 + q16 + 16u <= vend;
             const bool half = !full && b0 + q16 + 8u <= vend;  // sc % 8 == 0: valid length is a multiple of 8

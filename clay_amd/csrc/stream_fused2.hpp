@@ -147,9 +147,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                         const cu32p tj = tabc + zoff;
                         sfor<4>([&](auto rc) BS_INL {
                             constexpr int r = decltype(rc)::value;
-                            const GfTab tb = load_tab_c(tj + (r * 4 + j) * 8);
-                            U[r][0] ^= gf_mul_idx(i0, tb);
-                            U[r][1] ^= gf_mul_idx(i1, tb);
+                            if (uint32_t(r) < a.ne) {  // the erased rows only (uniform)
+                                const GfTab tb = load_tab_c(tj + (r * 4 + j) * 8);
+                                U[r][0] ^= gf_mul_idx(i0, tb);
+                                U[r][1] ^= gf_mul_idx(i1, tb);
+                            }
                         });
                     });
                     sfor<4>([&](auto rc) BS_INL {

@@ -179,9 +179,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_local(DecA
                 const GfIdx i0 = gf_idx(S[j * 8 + 2 * g]), i1 = gf_idx(S[j * 8 + 2 * g + 1]);
                 sfor<4>([&](auto rc) BS_INL {
                     constexpr int r = decltype(rc)::value;
-                    const GfTab tb = Kn::tab_at(tl, r * 4 + j);
-                    U[r][0] ^= gf_mul_idx(i0, tb);
-                    U[r][1] ^= gf_mul_idx(i1, tb);
+                    if (uint32_t(r) < ne) {  // the erased rows only (uniform)
+                        const GfTab tb = Kn::tab_at(tl, r * 4 + j);
+                        U[r][0] ^= gf_mul_idx(i0, tb);
+                        U[r][1] ^= gf_mul_idx(i1, tb);
+                    }
                 });
                 __builtin_amdgcn_sched_barrier(0);
             });
