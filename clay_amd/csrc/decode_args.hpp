@@ -41,15 +41,9 @@ struct DecArgs {
     uint32_t csh[4];
     int32_t g2;
     uint32_t x2;
-    // fused decode v2 (k_stream_fused2): target layers of iscore level l + 1 whose term is
-    // A_(Y,X) C(e_Y, z[Y:=X]) at bytes [gstart[16 l + 4 Y + X], gstart[.. + 1]) of the layer list
-    // (tabs + kDecZList bytes)
-    uint16_t gstart[68];
 };
 // local decode: v_perm table of det^-1 = (1 + gamma^2)^-1 (pair inversion, transforms.rs:108-125)
 constexpr int kDecDetInv = 80;
-// fused decode v2: byte offset of the per-level target-layer list in the tables buffer (<= 768)
-constexpr int kDecZList = 704 * 4;
 constexpr int kDecOrder = 640;
 // split solve: correction pairs (uint16 layer | Y << 8 | X << 10: C(e_Y, z[Y:=X]) feeds layer z)
 // from dword kDecPairs; at most 768 (4 erasures: 108 x 3 + 54 x 6 + 12 x 9 + 12)

@@ -2046,7 +2046,7 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
 
 hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
 
-// Fused decode v2 (stream_fused2.hpp): one erasure per y-section, one launch, rounds of tile k-1
+// Fused decode v2 (stream_fused2.hpp): one erasure in each y-section, one launch, rounds of tile k-1
 // on the loader waves while tile k streams.  Ring of 10 - ne node buffers + the S/C region.
 template <int KD>
 static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
@@ -2057,6 +2057,7 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     bool ok = false;
     Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
     if (e || !ok) return e;
+    if (a.ne != 4) return Error{};  // one erasure in every section (the rounds' target enumeration)
     const uint32_t RB = 10 - a.ne;  // the S/C region takes ne of the 10 node buffers of LDS
     // the loads of a step are issued during the step before it (the ring holds both), also
     // across tiles: section 3 of tile k and section 0 of tile k + 1
@@ -2066,24 +2067,6 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
         if (ny > RB || ny + nn > RB) return Error{};
     }
     a.ring = RB;
-    // per (level, Y, X): target layers z of that iscore level, red in section Y, X != x_e(Y) used
-    uint8_t *zl = reinterpret_cast<uint8_t *>(tabs.data()) + bs::kDecZList;
-    uint32_t nz = 0;
-    for (uint32_t lv = 0; lv < 4; lv++)
-        for (uint32_t gi = 0; gi < 16; gi++) {
-            a.gstart[lv * 16 + gi] = uint16_t(nz);
-            const uint32_t Y = gi >> 2, X = gi & 3u;
-            if (!a.emask[Y] || ((a.emask[Y] >> X) & 1u) || !((a.used >> (4 * Y + X)) & 1u)) continue;
-            const uint32_t xe = uint32_t(__builtin_ctz(a.emask[Y]));
-            for (uint32_t z = 0; z < 256; z++) {
-                uint32_t level = 0;
-                for (int y = 0; y < 4; y++) level += (a.emask[y] >> ((z >> (2 * (3 - y))) & 3u)) & 1u;
-                if (level != lv + 1 || ((z >> (2 * (3 - Y))) & 3u) != xe) continue;
-                if (nz >= 768) return Error{};
-                zl[nz++] = uint8_t(z);
-            }
-        }
-    a.gstart[64] = uint16_t(nz);
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
     a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
     e = dec_tables(cs, prop, tabs, stream, &a.tabs);

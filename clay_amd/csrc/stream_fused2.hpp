@@ -1,5 +1,5 @@
-// stream_fused2.hpp -- single-launch decode for q = 4, t = 4 codes with one erasure in each of up
-// to four y-sections (the BASELINE worst case {0,4,8,12}): every survivor byte read from HBM
+// stream_fused2.hpp -- single-launch decode for q = 4, t = 4 codes with one erasure in each of the
+// four y-sections (the BASELINE worst case {0,4,8,12}): every survivor byte read from HBM
 // once, every output byte written once, and the latency-bound iscore rounds (decode.rs:196-254)
 // of tile k-1 run on other waves while tile k streams.
 //
@@ -14,13 +14,14 @@
 //   * 4 loader waves issue every LDS-DMA (as in k_stream_syn) AND solve tile k-1 meanwhile: the
 //     round of iscore level y + 1 during section step y of tile k (term-parallel: one item per
 //     (target layer, section Y, node X) x 8 bytes, A_(Y,X) C(e_Y, z[Y:=X]) XORed into every C_r(z)
-//     with 64-bit LDS atomics; items grouped by (Y, X) so a wave's tables are uniform -> SGPRs);
+//     with 64-bit LDS atomics; a wave owns 3 of the 12 (Y, X) groups, their tables in registers,
+//     and enumerates a level's target layers arithmetically -- no memory access but LDS);
 //   * after the last round the compute waves read C(k-1) into registers, hand the region over
 //     (S'(k) in) and store C(k-1): stores come from waves that never wait on vmcnt, so the
 //     loaders' counted DMA waits see loads only;
 //   * six workgroup barriers per tile (four section steps, rounds done, region free), all waves.
-// Tables and the per-level target lists live in global memory (L2 / scalar cache): the ring and
-// the S/C region take all 160 KiB of LDS.
+// Tables live in global memory (scalar loads; the solver's in registers): the ring and the S/C
+// region take all 160 KiB of LDS.
 #pragma once
 
 #include "stream_decode.hpp"
@@ -62,7 +63,26 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         };
         issue_upto(RB);
-        const uint8_t *zl = reinterpret_cast<const uint8_t *>(a.tabs) + kDecZList;
+        // the rounds' work of this wave: groups g = li + 4 j (j < 3) of the 12 (section Y,
+        // node X != x_e(Y)) pairs, Y = g / 3, X = the (g % 3)-th digit other than x_e(Y); their
+        // A_(Y,X) tables loaded once into registers (tile-invariant, uniform)
+        uint32_t xe[4];
+#pragma unroll
+        for (int y = 0; y < 4; y++) xe[y] = uint32_t(__builtin_ctz(a.emask[y]));
+        GfTab tg[3][4];
+        uint32_t gY[3], gX[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const uint32_t g = uint32_t(li) + 4u * uint32_t(j), Y = g / 3u, kk = g % 3u;
+            gY[j] = Y;
+            gX[j] = kk + (kk >= xe[Y] ? 1u : 0u);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                tg[j][r] = load_tab_c(tabc + (16u + (4u * Y + gX[j]) * 4u + uint32_t(r)) * 8u);
+                asm volatile("" : "+v"(tg[j][r].w0), "+v"(tg[j][r].w1), "+v"(tg[j][r].w2), "+v"(tg[j][r].w3),
+                             "+v"(tg[j][r].w4));
+            }
+        }
         for (uint32_t k = 0; k <= ntile; k++) {
             for (int y = 0; y < 4; y++) {
                 if (k < ntile) {
@@ -73,31 +93,46 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 lds_barrier();  // B_y(k): step (k, y) landed; C(k-1) of level y visible
                 if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
                 if (k == 0 || (PROBE & 1)) continue;
-                // ---- round of iscore level y + 1 of tile k - 1 ----
-                const uint32_t lv = uint32_t(y);
-                for (uint32_t gi = uint32_t(li); gi < 16u; gi += uint32_t(Kn::LOADERS)) {
-                    const uint32_t g0 = a.gstart[lv * 16u + gi], g1 = a.gstart[lv * 16u + gi + 1u];
-                    if (g0 == g1) continue;  // uniform
-                    const uint32_t Y = gi >> 2, X = gi & 3u;
-                    const uint32_t xe = uint32_t(__builtin_ctz(a.emask[Y]));
-                    const uint32_t ry = uint32_t(a.rix[4u * Y + xe]);
-                    const uint32_t sh = 2u * (3u - Y);
-                    GfTab t[4];
+                // ---- round of iscore level L = y + 1 of tile k - 1: every target layer z of level L
+                // red in section Y adds A_(Y,X) C(e_Y, z[Y := X]); targets enumerated arithmetically
+                // (z_Y = x_e(Y), L - 1 of the other three sections red, base-3 digits for the rest)
+                const uint32_t L = uint32_t(y) + 1u;
+                const uint32_t nn = 4u - L, p3 = nn == 3u ? 27u : nn == 2u ? 9u : nn == 1u ? 3u : 1u;
+                const uint32_t nsub = (L == 1u || L == 4u) ? 1u : 3u;
 #pragma unroll
-                    for (int r = 0; r < 4; r++) t[r] = load_tab_c(tabc + (16u + (4u * Y + X) * 4u + uint32_t(r)) * 8u);
-                    const int32_t dz = (int32_t(X) - int32_t(xe)) * int32_t(1u << sh);  // z[Y := X] - z (z_Y = xe)
+                for (int j = 0; j < 3; j++) {
+                    const uint32_t Y = gY[j], X = gX[j];
+                    if (!((a.used >> (4u * Y + X)) & 1u)) continue;  // uniform
+                    const uint32_t ry = uint32_t(a.rix[4u * Y + xe[Y]]);
                     const uint8_t *src = scr + ry * BUF;
-                    for (uint32_t it = g0 * 8u + uint32_t(lane); it < g1 * 8u; it += 64u) {
-                        const uint32_t z = zl[it >> 3], d8 = (it & 7u) * 8u;
-                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + uint32_t(int32_t(z) + dz) * 64u + d8);
+                    for (uint32_t it = uint32_t(lane); it < nsub * p3 * 8u; it += 64u) {
+                        const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
+                        const uint32_t sub = ci / p3;
+                        uint32_t v = ci % p3;
+                        const uint32_t mask = L == 1u ? 0u : L == 2u ? (1u << sub) : L == 3u ? (7u ^ (4u >> sub)) : 7u;
+                        uint32_t z = xe[Y] * Kn::wt(int(Y)), zs = X * Kn::wt(int(Y)), o = 0;
+#pragma unroll
+                        for (int yy = 0; yy < 4; yy++) {
+                            if (uint32_t(yy) == Y) continue;
+                            uint32_t dgt;
+                            if ((mask >> o) & 1u) {
+                                dgt = xe[yy];
+                            } else {
+                                const uint32_t u = v % 3u;
+                                v /= 3u;
+                                dgt = u + (u >= xe[yy] ? 1u : 0u);
+                            }
+                            z += dgt * Kn::wt(yy);
+                            zs += dgt * Kn::wt(yy);
+                            o++;
+                        }
+                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + zs * 64u + d8);
                         const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
 #pragma unroll
                         for (int r = 0; r < 4; r++) {
-                            if (uint32_t(r) < a.ne) {
-                                const uint64_t v = uint64_t(gf_mul_idx(i0, t[r])) | (uint64_t(gf_mul_idx(i1, t[r])) << 32);
-                                __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + z * 64u + d8), v,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            }
+                            const uint64_t w = uint64_t(gf_mul_idx(i0, tg[j][r])) | (uint64_t(gf_mul_idx(i1, tg[j][r])) << 32);
+                            __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + z * 64u + d8), w,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
                 }

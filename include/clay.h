@@ -287,9 +287,9 @@ int clay_set_encode_path(int mode);
  *                streaming decode ("stream-split"); everything else as auto
  *   4 stream-fused -- as stream, but on the fused single-launch k_stream_decode ("stream")
  *   5 stream-local -- every decode the local kernel takes on it ("stream-local"); else as auto
- *   6 stream-fused2 -- decodes with one erasure per y-section on the fused decode v2
- *                (k_stream_fused2, "stream-fused2"; ring of 10 - e buffers for e erasures:
- *                any two neighbouring sections hold <= 10 - e surviving real nodes); else as auto
+ *   6 stream-fused2 -- decodes with one erasure in each y-section on the fused decode v2
+ *                (k_stream_fused2, "stream-fused2"; ring of 6 node buffers: any two
+ *                neighbouring sections hold <= 6 surviving real nodes); else as auto
  * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
  * (planner and executor tuning) are read once when the library is loaded.
  * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an

@@ -76,14 +76,15 @@ def test_bitsliced_encode_matches_oracle(oracle_mod, cfg, tile, scale):
     assert np.array_equal(got, ref), (cfg, tile, scale)
 
 
-STREAM3_SC = [16, 17, 100, 511, 512, 513, 1000, 4098, 512 * 256 + 37, 512 * 300 * 8 + 2, 3_314_018 // 64]
+# even: the reference pads to k * alpha * 2 (encode.rs:33-39); 2 mod 8 like the BASELINE chunk
+STREAM3_SC = [16, 18, 100, 510, 512, 514, 1000, 4098, 512 * 256 + 38, 512 * 300 * 8 + 2, 51_782]
 
 
 @pytest.mark.parametrize("loaders", [2, 7])
 @pytest.mark.parametrize("sc", STREAM3_SC)
 def test_stream3_encode_matches_oracle(oracle_mod, loaders, sc):
-    """(9,3,11) streaming kernel (stream_encode3.hpp): any sub-chunk size >= 16 (odd sizes, one
-    partial tile, 2 mod 8 rows like the 256 MiB BASELINE chunk, more tiles than workgroups),
+    """(9,3,11) streaming kernel (stream_encode3.hpp): sub-chunk sizes from 16 (one partial tile,
+    2 mod 8 rows like the 256 MiB BASELINE chunk, more tiles than workgroups),
     2 / 7 loader waves, bit-exact against the oracle."""
     c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
     n = 9 * c.sub_chunk_no * sc - 5
