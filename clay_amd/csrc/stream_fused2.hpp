@@ -14,8 +14,9 @@
 //   * 4 loader waves issue every LDS-DMA (as in k_stream_syn) AND solve tile k-1 meanwhile: the
 //     round of iscore level y + 1 during section step y of tile k (term-parallel: one item per
 //     (target layer, section Y, node X) x 8 bytes, A_(Y,X) C(e_Y, z[Y:=X]) XORed into every C_r(z)
-//     with 64-bit LDS atomics; a wave owns 3 of the 12 (Y, X) groups, their tables in registers,
-//     and enumerates a level's target layers arithmetically -- no memory access but LDS);
+//     with 64-bit LDS atomics; a wave owns one section Y: per target it sums the three X terms in
+//     registers (tables loaded once) and issues one atomic per row; a level's target layers are
+//     enumerated arithmetically -- no memory access but LDS);
 //   * after the last round the compute waves read C(k-1) into registers, hand the region over
 //     (S'(k) in) and store C(k-1): stores come from waves that never wait on vmcnt, so the
 //     loaders' counted DMA waits see loads only;
@@ -63,26 +64,24 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         };
         issue_upto(RB);
-        // the rounds' work of this wave: groups g = li + 4 j (j < 3) of the 12 (section Y,
-        // node X != x_e(Y)) pairs, Y = g / 3, X = the (g % 3)-th digit other than x_e(Y); their
-        // A_(Y,X) tables loaded once into registers (tile-invariant, uniform)
+        // the rounds' work of this wave: the targets red in section Y = li (one wave per section);
+        // the A_(Y,X) tables of its three X != x_e(Y), loaded once into registers (tile-invariant)
         uint32_t xe[4];
 #pragma unroll
         for (int y = 0; y < 4; y++) xe[y] = uint32_t(__builtin_ctz(a.emask[y]));
+        const uint32_t Y = uint32_t(li), xY = xe[Y];
         GfTab tg[3][4];
-        uint32_t gY[3], gX[3];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const uint32_t g = uint32_t(li) + 4u * uint32_t(j), Y = g / 3u, kk = g % 3u;
-            gY[j] = Y;
-            gX[j] = kk + (kk >= xe[Y] ? 1u : 0u);
+            const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                tg[j][r] = load_tab_c(tabc + (16u + (4u * Y + gX[j]) * 4u + uint32_t(r)) * 8u);
+                tg[j][r] = load_tab_c(tabc + (16u + (4u * Y + X) * 4u + uint32_t(r)) * 8u);
                 asm volatile("" : "+v"(tg[j][r].w0), "+v"(tg[j][r].w1), "+v"(tg[j][r].w2), "+v"(tg[j][r].w3),
                              "+v"(tg[j][r].w4));
             }
         }
+        const uint8_t *src = scr + uint32_t(a.rix[4u * Y + xY]) * BUF;  // C(e_Y, .)
         for (uint32_t k = 0; k <= ntile; k++) {
             for (int y = 0; y < 4; y++) {
                 if (k < ntile) {
@@ -94,47 +93,51 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
                 if (k == 0 || (PROBE & 1)) continue;
                 // ---- round of iscore level L = y + 1 of tile k - 1: every target layer z of level L
-                // red in section Y adds A_(Y,X) C(e_Y, z[Y := X]); targets enumerated arithmetically
-                // (z_Y = x_e(Y), L - 1 of the other three sections red, base-3 digits for the rest)
+                // red in section Y adds sum over X != x_e(Y) of A_(Y,X) C(e_Y, z[Y := X]) (the three
+                // terms summed in registers, one 64-bit LDS atomic per row); targets enumerated
+                // arithmetically (z_Y = x_e(Y), L - 1 of the other sections red, base-3 digits for
+                // the rest)
                 const uint32_t L = uint32_t(y) + 1u;
                 const uint32_t nn = 4u - L, p3 = nn == 3u ? 27u : nn == 2u ? 9u : nn == 1u ? 3u : 1u;
                 const uint32_t nsub = (L == 1u || L == 4u) ? 1u : 3u;
+                for (uint32_t it = uint32_t(lane); it < nsub * p3 * 8u; it += 64u) {
+                    const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
+                    const uint32_t sub = ci / p3;
+                    uint32_t v = ci % p3;
+                    const uint32_t mask = L == 1u ? 0u : L == 2u ? (1u << sub) : L == 3u ? (7u ^ (4u >> sub)) : 7u;
+                    uint32_t zb = 0, o = 0;  // z without section Y's digit
 #pragma unroll
-                for (int j = 0; j < 3; j++) {
-                    const uint32_t Y = gY[j], X = gX[j];
-                    if (!((a.used >> (4u * Y + X)) & 1u)) continue;  // uniform
-                    const uint32_t ry = uint32_t(a.rix[4u * Y + xe[Y]]);
-                    const uint8_t *src = scr + ry * BUF;
-                    for (uint32_t it = uint32_t(lane); it < nsub * p3 * 8u; it += 64u) {
-                        const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
-                        const uint32_t sub = ci / p3;
-                        uint32_t v = ci % p3;
-                        const uint32_t mask = L == 1u ? 0u : L == 2u ? (1u << sub) : L == 3u ? (7u ^ (4u >> sub)) : 7u;
-                        uint32_t z = xe[Y] * Kn::wt(int(Y)), zs = X * Kn::wt(int(Y)), o = 0;
-#pragma unroll
-                        for (int yy = 0; yy < 4; yy++) {
-                            if (uint32_t(yy) == Y) continue;
-                            uint32_t dgt;
-                            if ((mask >> o) & 1u) {
-                                dgt = xe[yy];
-                            } else {
-                                const uint32_t u = v % 3u;
-                                v /= 3u;
-                                dgt = u + (u >= xe[yy] ? 1u : 0u);
-                            }
-                            z += dgt * Kn::wt(yy);
-                            zs += dgt * Kn::wt(yy);
-                            o++;
+                    for (int yy = 0; yy < 4; yy++) {
+                        if (uint32_t(yy) == Y) continue;
+                        uint32_t dgt;
+                        if ((mask >> o) & 1u) {
+                            dgt = xe[yy];
+                        } else {
+                            const uint32_t u = v % 3u;
+                            v /= 3u;
+                            dgt = u + (u >= xe[yy] ? 1u : 0u);
                         }
-                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + zs * 64u + d8);
+                        zb += dgt * Kn::wt(yy);
+                        o++;
+                    }
+                    const uint32_t wy = Kn::wt(int(Y)), z = zb + xY * wy;
+                    uint32_t acc[4][2] = {};
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
+                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + (zb + X * wy) * 64u + d8);
                         const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
 #pragma unroll
                         for (int r = 0; r < 4; r++) {
-                            const uint64_t w = uint64_t(gf_mul_idx(i0, tg[j][r])) | (uint64_t(gf_mul_idx(i1, tg[j][r])) << 32);
-                            __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + z * 64u + d8), w,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            acc[r][0] ^= gf_mul_idx(i0, tg[j][r]);
+                            acc[r][1] ^= gf_mul_idx(i1, tg[j][r]);
                         }
                     }
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + z * 64u + d8),
+                                               uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
             lds_barrier();  // B_r(k): every atomic of tile k-1 done (lgkmcnt(0) before the barrier)

@@ -97,7 +97,7 @@ def test_host_api_concurrent_threads(oracle_mod, torch_cuda):
     assert not errors, errors
 
 
-@pytest.mark.parametrize("er,path", [([1, 5], "grouped"), ([0, 4, 8, 12], "stream-split")])
+@pytest.mark.parametrize("er,path", [([1, 2, 5, 6], "grouped"), ([0, 4, 8, 12], "stream-split")])
 def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path):
     """Decodes on 8 distinct, short-lived streams one after another reuse the pooled
     workspace (the grouped executor's U workspace, the split decode's S workspace): the pool
