@@ -126,12 +126,18 @@ static hipError_t launch_f2(const bs::DecArgs &a, hipStream_t stream, int dev) {
 hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev) {
 #ifdef CLAY_DECODE_PROBES
     const int probe = tuning().decode_probe;
-    if (kd == 10 && probe >= 31 && probe <= 39) {  // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only
+    // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only, 36 no rounds / presolve,
+    // 37 no rounds / stores, 38 no rounds / phase-A math (presolve kept), 39 no presolve
+    if (kd == 10 && probe >= 31 && probe <= 39) {
         switch (probe) {
         case 31: return launch_f2<10, 1>(a, stream, dev);
         case 32: return launch_f2<10, 2>(a, stream, dev);
         case 34: return launch_f2<10, 4>(a, stream, dev);
         case 35: return launch_f2<10, 13>(a, stream, dev);
+        case 36: return launch_f2<10, 9>(a, stream, dev);
+        case 37: return launch_f2<10, 3>(a, stream, dev);
+        case 38: return launch_f2<10, 5>(a, stream, dev);
+        case 39: return launch_f2<10, 8>(a, stream, dev);
         default: break;
         }
     }

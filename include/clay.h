@@ -273,7 +273,9 @@ int clay_set_encode_path(int mode);
  *                per-level executor; decodes of >= 3 erasures of q = 4, t = 4 codes
  *                ((10,4,13), (9,4,12)) in distinct y-sections with sc % 8 == 0, sc >= 512 run
  *                the split streaming decode (k_stream_syn + k_stream_solve, last path
- *                "stream-split"); decodes of those codes whose erasures lie in one y-section
+ *                "stream-split") -- with one erasure in every section (the BASELINE
+ *                {0,4,8,12}) the fused decode v2 instead (k_stream_fused2, "stream-fused2");
+ *                decodes of those codes whose erasures lie in one y-section
  *                plus at most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4},
  *                {0,1,2,3}, ...) run the single-launch local decode (k_stream_local,
  *                "stream-local")

@@ -418,7 +418,7 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("mode,path", [("auto", "stream-split"), ("grouped", "grouped")])
+@pytest.mark.parametrize("mode,path", [("auto", "stream-fused2"), ("stream", "stream-split"), ("grouped", "grouped")])
 def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda, mode, path):
     """BASELINE config 5 on random (non-codeword) chunks under the auto executor (the split
     streaming decode) and the grouped plan executor."""
@@ -460,7 +460,7 @@ def test_cfg5_10_4_13_1GiB_decode_4_erasures_codeword_incl_parity(oracle_mod, to
     c.decode_device([None if i in er else full[i] for i in range(14)], er,
                     [outs[i] if i in er else None for i in range(14)], chunk)
     torch.cuda.synchronize()
-    assert clay_amd.last_exec_path() == "stream-split"  # auto, 4 erasures
+    assert clay_amd.last_exec_path() == "stream-fused2"  # auto, one erasure in every section
     for e in er:
         assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
 

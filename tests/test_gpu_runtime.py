@@ -99,6 +99,14 @@ def test_host_api_concurrent_threads(oracle_mod, torch_cuda):
 
 @pytest.mark.parametrize("er,path", [([1, 2, 5, 6], "grouped"), ([0, 4, 8, 12], "stream-split")])
 def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path):
+    prev = clay_amd.set_exec_mode("stream" if path == "stream-split" else "auto")
+    try:
+        _workspace_pool_reuse(oracle_mod, torch_cuda, er, path)
+    finally:
+        clay_amd.set_exec_mode(prev)
+
+
+def _workspace_pool_reuse(oracle_mod, torch_cuda, er, path):
     """Decodes on 8 distinct, short-lived streams one after another reuse the pooled
     workspace (the grouped executor's U workspace, the split decode's S workspace): the pool
     does not grow per stream (it grew by one workspace per stream handle before the pool
@@ -429,12 +437,21 @@ def test_capture_arena_reclaimed(oracle_mod, torch_cuda):
         clay_amd.release_captured(0)
 
 
-def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda):
-    """A 4-erasure (10,4,13) decode on the split streaming decode inside a stream capture: the
-    reserved workspace covers its S' lease and one eager call of the pattern prepared its
-    tables, so the capture allocates nothing (the pool does not grow) and replays bit-exact on
-    new data.  A pattern never run before fails inside the capture with a clear error instead
-    of invalidating it."""
+@pytest.mark.parametrize("mode,path", [("stream", "stream-split"), ("auto", "stream-fused2")])
+def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda, mode, path):
+    """A 4-erasure (10,4,13) decode inside a stream capture, on the split streaming decode (its S'
+    workspace lease covered by the reserved workspace) and on the fused decode v2 (no workspace):
+    one eager call of the pattern prepared its tables, so the capture allocates nothing (the pool
+    does not grow) and replays bit-exact on new data.  A pattern never run before fails inside the
+    capture with a clear error instead of invalidating it."""
+    prev = clay_amd.set_exec_mode(mode)
+    try:
+        _decode_graph_capture(oracle_mod, torch_cuda, path)
+    finally:
+        clay_amd.set_exec_mode(prev)
+
+
+def _decode_graph_capture(oracle_mod, torch_cuda, path):
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     sc = 1024
@@ -451,7 +468,7 @@ def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda):
     args = ([None if j in er else full[j] for j in range(14)], er, [outs[j] if j in er else None for j in range(14)])
     c.decode_device(*args, chunk, 0, st.cuda_stream)  # prepares the pattern's tables
     st.synchronize()
-    assert clay_amd.last_exec_path() == "stream-split"
+    assert clay_amd.last_exec_path() == path
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=st):
         c.decode_device(*args, chunk, 0, torch.cuda.current_stream().cuda_stream)
