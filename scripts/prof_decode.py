@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One decode (10,4,13) 1 GiB with 4 erasures {0,4,8,12} (and optionally repair (9,3,11)),
 repeated --iters times, for rocprofv3 --pmc passes (HBM bytes per launch; CLAY_EXEC picks the
-executor: auto = split streaming decode for >= 3 erasures of q = t = 4 codes, else the grouped
+executor: auto = the fused decode v2 for {0,4,8,12} (one erasure per section), else the grouped
 executor / bs-repair; stream = streaming decode for every eligible pattern)."""
 import argparse
 import os
