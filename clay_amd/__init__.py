@@ -109,7 +109,8 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
-_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-fused": 4, "stream-local": 5, "stream-fused2": 6}
+_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-fused": 4, "stream-local": 5, "stream-fused2": 6,
+               "codeword": 7}
 
 
 def set_exec_mode(mode: str) -> str:
@@ -118,8 +119,13 @@ def set_exec_mode(mode: str) -> str:
     q = 4, t = 4 codes; the bit-sliced repair kernels for q = m repairs from all n - 1 nodes),
     'grouped' (one launch per level), 'tile', 'stream' (the split streaming decode for every
     eligible q = 4, t = 4 decode, else as auto), 'stream-fused' (as 'stream' on the fused
-    single-launch decode kernel) or 'stream-local' (the local decode for patterns with erasures
-    in one y-section plus at most one other, which auto also runs).  Every mode produces the reference's bytes.  Returns the previous mode."""
+    single-launch decode kernel), 'stream-local' (the local decode for patterns with erasures
+    in one y-section plus at most one other, which auto also runs), 'stream-fused2' (the fused
+    decode v2 for one erasure in every y-section, which auto also runs) or 'codeword' (as auto,
+    and a single erasure with every other chunk present in a q = m code is rebuilt by the repair
+    kernel, reading 1/q of each chunk: the reference's bytes whenever the chunks are one
+    codeword, NOT on arbitrary inputs).  Every other mode produces the reference's bytes on any
+    input.  Returns the previous mode."""
     if mode not in _EXEC_MODES:
         raise ValueError(f"unknown exec mode {mode!r}")
     prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])

@@ -264,8 +264,8 @@ struct BsRepair {
 //    of NB buffers.  Loads of a tile in step order: the real nodes of every section y != Y0
 //    (one step each: PRT + transpose + fold into the Q accumulators), then the nodes of section Y0
 //    other than the lost one (the output step, phase 3).
-//  * Row r's 16-byte piece k sits at slot k ^ swz(r) (PARTS = 8: odd rows swapped halves), so a
-//    wave's ds_read_b128 of own and companion rows are bank-conflict free.
+//  * Row r's 16-byte piece k sits at slot k ^ swz(r) (PARTS = 8: odd rows swapped halves; PARTS =
+//    4: rows with bit 1 set), so a wave's ds_read_b128 of own rows are bank-conflict free.
 //  * The last tile of a sub-chunk may be partial (any length >= 16 bytes): its DMA reads a piece
 //    straddling the end from end - 16, the loader rewrites that piece in LDS byte by byte once it
 //    landed, and compute lanes store only the bytes inside the sub-chunk.
@@ -289,7 +289,7 @@ struct BsRepairStream {
     static constexpr int LDS_BYTES = NB * NODE;
     static constexpr int BPL = NBLK / LOADERS;  // blocks per loader wave per node
     static_assert(NBLK % LOADERS == 0, "node blocks split evenly over the loader waves");
-    static_assert(PARTS == 8 || PARTS == 16, "piece swizzle derived for 8 / 16 parts");
+    static_assert(PARTS == 4 || PARTS == 8 || PARTS == 16, "piece swizzle derived for 4 / 8 / 16 parts");
     static_assert(1024 % W == 0, "whole rows per DMA block");
     static constexpr int RPB = 1024 / W;  // rows per DMA block
 
@@ -310,7 +310,11 @@ struct BsRepairStream {
     }
     static constexpr int NT = soff(T);
     static_assert(NB >= 2 * Q && NT >= 1, "ring: two steps' loads in flight");
-    __host__ __device__ static constexpr uint32_t swz(uint32_t r) { return PARTS == 8 ? (r & 1u) * 8u : 0u; }
+    // PARTS = 4 (128-byte rows): rows with bit 1 set swap halves, so the 4 rows of a ds_read_b128
+    // lane group ({0-3, 12-15, 20-27}, ...) hit 4 distinct 16-bank quarters
+    __host__ __device__ static constexpr uint32_t swz(uint32_t r) {
+        return PARTS == 8 ? (r & 1u) * 8u : PARTS == 4 ? ((r >> 1) & 1u) * 4u : 0u;
+    }
 
     // node of tile-relative load q (x0 = the lost node's x: skipped in section Y0)
     __device__ static int node_of(int q, uint32_t x0) {

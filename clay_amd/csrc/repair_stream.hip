@@ -72,9 +72,11 @@ static hipError_t launch_km(int y0, const bs::RepArgs &a, hipStream_t stream, in
                 break;
             }
             if (e != hipErrorNotSupported) return e;
+            if (stream_mode == 3) return hipErrorNotSupported;  // streaming kernel only
             *launches = 1;
         }
     }
+    if (stream_mode == 3) return hipErrorNotSupported;
     switch (y0) {
     case 0: return launch_one<KD, M, 0>(a, stream);
     case 1: return launch_one<KD, M, 1>(a, stream);
@@ -86,17 +88,21 @@ static hipError_t launch_km(int y0, const bs::RepArgs &a, hipStream_t stream, in
 }
 
 // stream_mode: 0 = direct kernel, 1 = streaming kernel when the sub-chunk gives every CU a
-// tile, 2 = streaming kernel whenever the code has one.  Returns 1 = direct kernel launched,
-// 2 = streaming kernel launched, 0 = no instantiation for (k, m), < 0 = HIP error; *launches =
-// kernel launches issued (the streaming kernel adds one for a sub-chunk remainder).
+// tile, 2 = streaming kernel whenever the code has one, 3 = the streaming kernel when the
+// sub-chunk gives every CU a tile, else nothing.  Returns 1 = direct kernel launched, 2 =
+// streaming kernel launched, 0 = no instantiation for (k, m) (or none launched in mode 3), < 0 =
+// HIP error; *launches = kernel launches issued.
 int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream, int dev, int cus,
                             int stream_mode, int *launches) {
     hipError_t e;
     bool streamed = false;
     if (k == 9 && m == 3) e = launch_km<9, 3, 16, 7>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
-    else if (k == 10 && m == 4) e = launch_km<10, 4, 8, 4>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
+    // (10,4): 128-byte tiles (12.8 per CU on the 1 GiB stripe's 419,432-byte sub-chunks; 256-byte
+    // tiles: 6.4 per CU and a longer tail, 0.161 vs 0.139 ms, profiles/r04/repair/)
+    else if (k == 10 && m == 4) e = launch_km<10, 4, 4, 4>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
     else if (k == 4 && m == 2) e = launch_km<4, 2, 0, 0>(y0, a, stream, dev, cus, stream_mode, &streamed, launches);
     else return 0;
+    if (e == hipErrorNotSupported && stream_mode == 3) return 0;
     if (e != hipSuccess) return -int(e);
     return streamed ? 2 : 1;
 }

@@ -141,6 +141,9 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 }
             }
             lds_barrier();  // B_r(k): every atomic of tile k-1 done (lgkmcnt(0) before the barrier)
+            // the compute waves are past phase A(k): every ring buffer is free, so the next tile's
+            // first RB loads stream during the presolve, the region hand-over and the stores
+            if (k + 1u < ntile) issue_upto((k + 1u) * NT + RB);
             lds_barrier();  // B_w(k): the compute waves hold C(k-1); the region takes S'(k)
         }
         wait_vm0();
@@ -161,7 +164,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
             Kn::template phase_a<(PROBE & 4) ? 2 : 0>(a, smem, k * NT, c0, poff0, xeG, S, RB);
-            // bit planes -> bytes, then S' = H_K^-1 S per slot (tables: scalar loads)
+            // bit planes -> bytes
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 uint32_t v[8];
@@ -171,39 +174,47 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
 #pragma unroll
                 for (int w = 0; w < 8; w++) S[j * 8 + w] = v[w];
             }
-            if constexpr (!(PROBE & 8)) {
-                sfor<4>([&](auto gc) BS_INL {
-                    constexpr int g = decltype(gc)::value;
-                    uint32_t U[4][2] = {};
-                    sfor<4>([&](auto jc) BS_INL {
-                        constexpr int j = decltype(jc)::value;
-                        const GfIdx i0 = gf_idx(S[j * 8 + 2 * g]), i1 = gf_idx(S[j * 8 + 2 * g + 1]);
-                        // an opaque base per (g, j): the 4 tables are loaded here, not all 16 hoisted
-                        // out of the tile loop into SGPRs (which spilled into VGPR lanes)
-                        uint32_t zoff = 0;
-                        asm volatile("" : "+s"(zoff));
-                        const cu32p tj = tabc + zoff;
-                        sfor<4>([&](auto rc) BS_INL {
-                            constexpr int r = decltype(rc)::value;
-                            if (uint32_t(r) < a.ne) {  // the erased rows only (uniform)
-                                const GfTab tb = load_tab_c(tj + (r * 4 + j) * 8);
-                                U[r][0] ^= gf_mul_idx(i0, tb);
-                                U[r][1] ^= gf_mul_idx(i1, tb);
-                            }
-                        });
-                    });
-                    sfor<4>([&](auto rc) BS_INL {
-                        constexpr int r = decltype(rc)::value;
-                        S[r * 8 + 2 * g] = U[r][0];
-                        S[r * 8 + 2 * g + 1] = U[r][1];
-                    });
-                });
-            }
         } else {
 #pragma unroll
             for (int y = 0; y < 4; y++) lds_barrier();  // B_y(ntile): the last tile's rounds
         }
         lds_barrier();  // B_r(k): C(k-1) complete in the region
+        // S' = H_K^-1 S per slot (tables: scalar loads), after B_r(k) so the loaders stream
+        if (k < ntile && !(PROBE & 8)) {
+            // check j outer: its 4 tables (rows r) are loaded once per tile and serve the 4 slots
+            // (16 table loads per tile instead of 64; an opaque base per j keeps them from being
+            // hoisted out of the tile loop into SGPRs that spill)
+            uint32_t U[4][4][2] = {};  // [slot g][row r][word]
+            sfor<4>([&](auto jc) BS_INL {
+                constexpr int j = decltype(jc)::value;
+                uint32_t zoff = 0;
+                asm volatile("" : "+s"(zoff));
+                const cu32p tj = tabc + zoff;
+                GfTab tb[4];
+                sfor<4>([&](auto rc) BS_INL {
+                    constexpr int r = decltype(rc)::value;
+                    if (uint32_t(r) < a.ne) tb[r] = load_tab_c(tj + (r * 4 + j) * 8);  // erased rows only
+                });
+                sfor<4>([&](auto gc) BS_INL {
+                    constexpr int g = decltype(gc)::value;
+                    const GfIdx i0 = gf_idx(S[j * 8 + 2 * g]), i1 = gf_idx(S[j * 8 + 2 * g + 1]);
+                    sfor<4>([&](auto rc) BS_INL {
+                        constexpr int r = decltype(rc)::value;
+                        if (uint32_t(r) < a.ne) {  // uniform
+                            U[g][r][0] ^= gf_mul_idx(i0, tb[r]);
+                            U[g][r][1] ^= gf_mul_idx(i1, tb[r]);
+                        }
+                    });
+                });
+            });
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    S[r * 8 + 2 * g] = U[g][r][0];
+                    S[r * 8 + 2 * g + 1] = U[g][r][1];
+                }
+        }
         // C(k-1) -> registers: 1,024 rows x 64 B, lane = one 16-byte piece of 16 rows per pass
         uint4 ov[8];
         if (k >= 1) {

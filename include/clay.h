@@ -292,10 +292,18 @@ int clay_set_encode_path(int mode);
  *   6 stream-fused2 -- decodes with one erasure in each y-section on the fused decode v2
  *                (k_stream_fused2, "stream-fused2"; ring of 6 node buffers: any two
  *                neighbouring sections hold <= 6 surviving real nodes); else as auto
+ *   7 codeword -- as auto, for callers whose chunks are one codeword (the crate's usage: chunks
+ *                it encoded): a decode of ONE erased node with every other node present, in a
+ *                q = m code ((9,3,11), (10,4,13)), is rebuilt by k_bs_repair_stream from the whole
+ *                chunks ("bs-repair-stream"; when the sub-chunk gives every CU a tile), reading the
+ *                alpha / q layers of the node's repair plane of each chunk instead of every layer
+ *                ((10,4,13) 1 GiB {0}: 0.16 ms vs 0.39 on the local decode).  On a codeword the
+ *                bytes equal decode.rs's (the codeword through k chunks is unique); on inputs that
+ *                are not a codeword they differ, which is why auto keeps the decode.
  * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
  * (planner and executor tuning) are read once when the library is loaded.
- * Every mode produces the reference's bytes.  Returns the previous mode, or -1 for an
- * unknown mode (setting unchanged). */
+ * Every mode but codeword produces the reference's bytes on any input; codeword does on
+ * codewords.  Returns the previous mode, or -1 for an unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
  * "tile" (k_texec), "grouped" (k_gexec), "stream-split" (k_stream_syn + k_stream_solve),

@@ -154,6 +154,12 @@ if __name__ == "__main__":
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4])),
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 2, 3])),
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [12])),
+            # exec mode "codeword": one erasure rebuilt by the repair kernel from whole chunks
+            # (algorithmic bytes still counted as a decode's: every survivor + the output)
+            ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [0], "codeword")),
+            ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [12], "codeword")),
+            ("codeword", lambda: decode_cfg(9, 3, 11, 9 * (256 << 20), [0])),
+            ("codeword", lambda: decode_cfg(9, 3, 11, 9 * (256 << 20), [0], "codeword")),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 0)),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 11)),
             ("repair", lambda: repair_cfg(10, 4, 13, 107_374_592, 0)),

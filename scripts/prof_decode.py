@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One decode (10,4,13) 1 GiB with 4 erasures {0,4,8,12} (and optionally repair (9,3,11)),
+"""One decode (10,4,13) 1 GiB with erasures --er (default {0,4,8,12}) (and optionally repair (9,3,11)),
 repeated --iters times, for rocprofv3 --pmc passes (HBM bytes per launch; CLAY_EXEC picks the
 executor: auto = the fused decode v2 for {0,4,8,12} (one erasure per section), else the grouped
 executor / bs-repair; stream = streaming decode for every eligible pattern)."""
@@ -18,11 +18,12 @@ clay_amd.set_exec_mode(os.environ.get("CLAY_EXEC", "auto"))  # auto | grouped | 
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--what", default="decode4")
+ap.add_argument("--er", default="0,4,8,12", help="erasures of the decode (e.g. 0 for the local decode)")
 args = ap.parse_args()
 if args.what == "decode4":
     c = ClayCode(10, 4, 13)
     chunk = c.encoded_chunk_size(1 << 30)
-    er = [0, 4, 8, 12]
+    er = [int(x) for x in args.er.split(",")]
     full = torch.randint(0, 256, (c.n, chunk), dtype=torch.uint8, device="cuda")
     outs = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
     ins = [None if i in er else full[i] for i in range(c.n)]

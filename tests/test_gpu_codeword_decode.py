@@ -1,0 +1,80 @@
+"""GPU tests of exec mode "codeword": a decode of one erased node with every other chunk present,
+in a q = m code, is rebuilt by the streaming repair kernel (k_bs_repair_stream) from the whole
+chunks.  The reference's decode (decode.rs:31-161) and repair (repair.rs:140-421) return the same
+bytes whenever the chunks are one codeword, so the inputs here are codewords encoded by the oracle
+and every rebuilt chunk (data or parity) must equal the encoded one bit for bit.  Other patterns
+and sizes run as in auto."""
+import numpy as np
+import pytest
+
+import clay_amd
+from clay_amd import ClayCode
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def codeword_mode():
+    prev = clay_amd.set_exec_mode("codeword")
+    yield
+    clay_amd.set_exec_mode(prev)
+
+
+def _decode_dev(torch, c, full, er, chunk):
+    outs = torch.full((c.n, chunk), 0xA5, dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(c.n)], er,
+                    [outs[i] if i in er else None for i in range(c.n)], chunk)
+    torch.cuda.synchronize()
+    return outs
+
+
+# sub-chunks that give every CU of a 256-CU MI355X at least one tile of the streaming repair
+# kernel (256 B for (10,4,13), 512 B for (9,3,11)), ragged ends included (sc = 2 mod 8 for (9,3,11))
+@pytest.mark.parametrize("cfg,sc,lost", [((10, 4, 13), 65536 + 40, [0, 5, 9, 10, 13]),
+                                         ((9, 3, 11), 131072 + 2, [0, 4, 8, 11])])
+def test_codeword_single_erasure_runs_repair(oracle_mod, torch_cuda, codeword_mode, cfg, sc, lost):
+    torch = torch_cuda
+    c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
+    chunk = c.sub_chunk_no * sc
+    ref = o.encode_array(np.random.default_rng(sc).integers(0, 256, c.k * chunk, dtype=np.uint8))
+    full = torch.from_numpy(ref).cuda()
+    for e in lost:
+        outs = _decode_dev(torch, c, full, [e], chunk)
+        assert clay_amd.last_exec_path() == "bs-repair-stream", (e, clay_amd.last_exec_path())
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (cfg, e)
+        # the other outputs were not requested and stay untouched
+        assert int((outs[(e + 1) % c.n] != 0xA5).sum().item()) == 0
+
+
+def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda, codeword_mode):
+    """Two erasures, and one erasure at a sub-chunk too small for every CU to get a tile: the
+    paths auto takes (local decode), bit-exact."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    for sc, er in ((65536 + 40, [0, 4]), (64 * 40 + 8, [3])):
+        chunk = c.sub_chunk_no * sc
+        ref = o.encode_array(np.random.default_rng(sc + len(er)).integers(0, 256, c.k * chunk, dtype=np.uint8))
+        full = torch.from_numpy(ref).cuda()
+        outs = _decode_dev(torch, c, full, er, chunk)
+        assert clay_amd.last_exec_path() == "stream-local", (sc, er, clay_amd.last_exec_path())
+        for e in er:
+            assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (sc, er, e)
+
+
+def test_auto_keeps_decode_semantics_on_non_codewords(oracle_mod, torch_cuda):
+    """auto never takes the repair route: on random (non-codeword) chunks a single-erasure decode
+    at the same size still returns the reference decode's bytes."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    sc = 65536 + 40
+    chunk = c.sub_chunk_no * sc
+    chunks = np.random.default_rng(3).integers(0, 256, (c.n, chunk), dtype=np.uint8)
+    prev = clay_amd.set_exec_mode("auto")
+    try:
+        outs = _decode_dev(torch, c, torch.from_numpy(chunks).cuda(), [2], chunk)
+        assert clay_amd.last_exec_path() == "stream-local"
+    finally:
+        clay_amd.set_exec_mode(prev)
+    av = {i: chunks[i] for i in range(c.n) if i != 2}
+    ref = np.frombuffer(o.decode(av, [2]), dtype=np.uint8).reshape(c.k, -1)
+    assert np.array_equal(outs[2].cpu().numpy(), ref[2])

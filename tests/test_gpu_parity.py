@@ -262,7 +262,7 @@ def test_small_decode_plan_executor(oracle_mod, mode, expect):
 def test_exec_mode_rejects_unknown():
     with pytest.raises(ValueError):
         clay_amd.set_exec_mode("fused")
-    assert clay_amd._lib.lib().clay_set_exec_mode(7) == -1
+    assert clay_amd._lib.lib().clay_set_exec_mode(8) == -1
 
 
 def test_repair_with_all_helpers_and_aloof(oracle_mod):
