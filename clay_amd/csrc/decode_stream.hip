@@ -128,8 +128,11 @@ hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t
     const int probe = tuning().decode_probe;
     // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only, 36 no rounds / presolve,
     // 37 no rounds / stores, 38 no rounds / phase-A math (presolve kept), 39 no presolve
-    if (kd == 10 && probe >= 31 && probe <= 39) {
+    // 40: the full kernel with s_memtime segment timing (workgroup 0 prints its compute wave 0 and
+    // loader wave 0 totals)
+    if (kd == 10 && probe >= 31 && probe <= 40) {
         switch (probe) {
+        case 40: return launch_f2<10, 16>(a, stream, dev);
         case 31: return launch_f2<10, 1>(a, stream, dev);
         case 32: return launch_f2<10, 2>(a, stream, dev);
         case 34: return launch_f2<10, 4>(a, stream, dev);

@@ -206,12 +206,19 @@ struct StreamDec {
     // S (4 checks x 8 planes, the lane's 4 layers x 8 positions) += sum_i H_i U'(i) + H_e Out(e);
     // section Y's alive nodes are loads qbase + sec_off[Y] .. of the ring (buffer = load % ring).
     // RT (k_stream_local): column digits at a.csh[y], and any number of erased nodes in section G
+    // tbar (timing probe of k_stream_fused2 only): cycles spent in the four step barriers
     template <int PROBE, bool RT = false>
     __device__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
-                                   uint32_t (&S)[32], uint32_t R) {  // R: ring depth (node buffers)
+                                   uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {  // R: ring depth
         sfor<4>([&](auto yc) BS_INL {
             constexpr int Y = decltype(yc)::value;
-            lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
+            if (tbar) {
+                const uint64_t t0 = __builtin_amdgcn_s_memtime();
+                lds_barrier();
+                *tbar += __builtin_amdgcn_s_memtime() - t0;
+            } else {
+                lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
+            }
             if constexpr ((PROBE & 2) != 0) return;
             const uint32_t c = opq(c0), poff = opq(poff0);
             const uint32_t aliveY = (a.alive >> (4 * Y)) & 15u;

@@ -31,7 +31,8 @@ namespace clay {
 namespace bs {
 
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
-// 2 = no output stores, 4 = no phase-A math, 8 = no presolve
+// 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
+// (workgroup 0 prints the totals of compute wave 0 and loader wave 0)
 template <int KD, int G, int PROBE = 0>
 __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(DecArgs a) {
     using Kn = StreamDec<KD, G>;
@@ -82,14 +83,28 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         }
         const uint8_t *src = scr + uint32_t(a.rix[4u * Y + xY]) * BUF;  // C(e_Y, .)
+        constexpr bool TM = (PROBE & 16) != 0;
+        uint64_t tm_vm = 0, tm_bar = 0, tm_rnd = 0, tm_end = 0, t0 = 0;
+        const uint64_t tm_start = TM ? __builtin_amdgcn_s_memtime() : 0;
         for (uint32_t k = 0; k <= ntile; k++) {
             for (int y = 0; y < 4; y++) {
+                if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
                 if (k < ntile) {
                     // loads of step (k, y) landed; the loads issued after them may stay in flight
                     const uint32_t qend = k * NT + a.sec_off[y + 1];
                     wait_vm_rt(int((issued - qend) * uint32_t(Kn::BPL)));
                 }
+                if constexpr (TM) {
+                    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                    tm_vm += t1 - t0;
+                    t0 = t1;
+                }
                 lds_barrier();  // B_y(k): step (k, y) landed; C(k-1) of level y visible
+                if constexpr (TM) {
+                    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                    tm_bar += t1 - t0;
+                    t0 = t1;
+                }
                 if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
                 if (k == 0 || (PROBE & 1)) continue;
                 // ---- round of iscore level L = y + 1 of tile k - 1: every target layer z of level L
@@ -139,14 +154,23 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                                                uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
             }
+            if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
             lds_barrier();  // B_r(k): every atomic of tile k-1 done (lgkmcnt(0) before the barrier)
             // the compute waves are past phase A(k): every ring buffer is free, so the next tile's
             // first RB loads stream during the presolve, the region hand-over and the stores
             if (k + 1u < ntile) issue_upto((k + 1u) * NT + RB);
             lds_barrier();  // B_w(k): the compute waves hold C(k-1); the region takes S'(k)
+            if constexpr (TM) tm_end += __builtin_amdgcn_s_memtime() - t0;
         }
         wait_vm0();
+        if constexpr (TM) {
+            if (blockIdx.x == 0 && li == 0 && lane == 0)
+                printf("f2-timing loader tiles %u total %lu vmwait %lu barrier %lu rounds %lu br+bw %lu\n", ntile,
+                       (unsigned long)(__builtin_amdgcn_s_memtime() - tm_start), (unsigned long)tm_vm,
+                       (unsigned long)tm_bar, (unsigned long)tm_rnd, (unsigned long)tm_end);
+        }
         return;
     }
 
@@ -154,8 +178,12 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
     const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
     const uint32_t emG = a.emask[G];
     const int xeG = emG ? __builtin_ctz(emG) : -1;
+    constexpr bool TM = (PROBE & 16) != 0;
+    uint64_t tm_pa = 0, tm_pabar = 0, tm_pre = 0, tm_br = 0, tm_rd = 0, tm_bw = 0, tm_st = 0, t0 = 0;
+    const uint64_t tm_start = TM ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t k = 0; k <= ntile; k++) {
         uint32_t S[32];
+        if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
         if (k < ntile) {
             const typename Kn::Tile t = tm.tile(k, wslot, ns);
             const bool straddle = t.vend < t.b0 + uint32_t(Kn::W) && ((t.vend - t.b0) & 15u) == 8u;
@@ -163,7 +191,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
-            Kn::template phase_a<(PROBE & 4) ? 2 : 0>(a, smem, k * NT, c0, poff0, xeG, S, RB);
+            Kn::template phase_a<(PROBE & 4) ? 2 : 0>(a, smem, k * NT, c0, poff0, xeG, S, RB, TM ? &tm_pabar : nullptr);
             // bit planes -> bytes
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -178,7 +206,17 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
 #pragma unroll
             for (int y = 0; y < 4; y++) lds_barrier();  // B_y(ntile): the last tile's rounds
         }
+        if constexpr (TM) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tm_pa += t1 - t0;
+            t0 = t1;
+        }
         lds_barrier();  // B_r(k): C(k-1) complete in the region
+        if constexpr (TM) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tm_br += t1 - t0;
+            t0 = t1;
+        }
         // S' = H_K^-1 S per slot (tables: scalar loads), after B_r(k) so the loaders stream
         if (k < ntile && !(PROBE & 8)) {
             // check j outer: its 4 tables (rows r) are loaded once per tile and serve the 4 slots
@@ -215,6 +253,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     S[r * 8 + 2 * g + 1] = U[g][r][1];
                 }
         }
+        if constexpr (TM) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tm_pre += t1 - t0;
+            t0 = t1;
+        }
         // C(k-1) -> registers: 1,024 rows x 64 B, lane = one 16-byte piece of 16 rows per pass
         uint4 ov[8];
         if (k >= 1) {
@@ -223,7 +266,17 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 if (uint32_t(i >> 1) < a.ne)  // rows of the region: ne (it holds ne x 16 KiB)
                     ov[i] = *reinterpret_cast<const uint4 *>(scr + (uint32_t(i) * 512u + threadIdx.x) * 16u);
         }
+        if constexpr (TM) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tm_rd += t1 - t0;
+            t0 = t1;
+        }
         lds_barrier();  // B_w(k): the region is free
+        if constexpr (TM) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tm_bw += t1 - t0;
+            t0 = t1;
+        }
         if (k < ntile) {
             const uint32_t z0 = Kn::layer0(opq(c0));
 #pragma unroll
@@ -251,6 +304,15 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 else if (half) *reinterpret_cast<uint2 *>(o) = make_uint2(ov[i].x, ov[i].y);
             }
         }
+        if constexpr (TM) tm_st += __builtin_amdgcn_s_memtime() - t0;
+    }
+    if constexpr (TM) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            printf("f2-timing compute tiles %u total %lu phaseA %lu (barriers %lu) B_r %lu presolve %lu Cread %lu B_w %lu "
+                   "Swrite+stores %lu\n",
+                   ntile, (unsigned long)(__builtin_amdgcn_s_memtime() - tm_start), (unsigned long)tm_pa,
+                   (unsigned long)tm_pabar, (unsigned long)tm_br, (unsigned long)tm_pre, (unsigned long)tm_rd,
+                   (unsigned long)tm_bw, (unsigned long)tm_st);
     }
 }
 
