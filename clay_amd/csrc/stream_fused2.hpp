@@ -30,6 +30,12 @@
 namespace clay {
 namespace bs {
 
+// solver work items per lane and round: level 1 and 2 have 27 targets x 8 pieces (4 passes of 64
+// lanes), level 3 9 x 8 (2), level 4 1 x 8 (1)
+constexpr int kF2Iters[4] = {4, 4, 2, 1};
+constexpr int kF2Off[4] = {0, 4, 8, 10};
+constexpr int kF2Items = 11;
+
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
 // 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
 // (workgroup 0 prints the totals of compute wave 0 and loader wave 0)
@@ -83,11 +89,47 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         }
         const uint8_t *src = scr + uint32_t(a.rix[4u * Y + xY]) * BUF;  // C(e_Y, .)
+        const uint32_t wy64 = Kn::wt(int(Y)) * 64u;
+        // the lane's work items of every round, tile-invariant: byte offset (layer without section
+        // Y's digit) x 64 + 8-byte piece, ~0 = none.  Level L's targets: z_Y = x_e(Y), L - 1 of the
+        // other sections red (sub-set `sub` of the C(3, L - 1)), base-3 digits for the rest.
+        uint32_t rb[kF2Items];
+        sfor<4>([&](auto yc) BS_INL {
+            constexpr int y = decltype(yc)::value;
+            constexpr uint32_t L = uint32_t(y) + 1u, nn = 4u - L;
+            constexpr uint32_t p3 = nn == 3u ? 27u : nn == 2u ? 9u : nn == 1u ? 3u : 1u;
+            constexpr uint32_t nsub = (L == 1u || L == 4u) ? 1u : 3u;
+#pragma unroll
+            for (int i = 0; i < kF2Iters[y]; i++) {
+                const uint32_t it = uint32_t(lane) + 64u * uint32_t(i);
+                const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
+                const uint32_t sub = ci / p3;
+                uint32_t v = ci % p3;
+                const uint32_t mask = L == 1u ? 0u : L == 2u ? (1u << sub) : L == 3u ? (7u ^ (4u >> sub)) : 7u;
+                uint32_t zb = 0, o = 0;
+#pragma unroll
+                for (int yy = 0; yy < 4; yy++) {
+                    if (uint32_t(yy) == Y) continue;
+                    uint32_t dgt;
+                    if ((mask >> o) & 1u) {
+                        dgt = xe[yy];
+                    } else {
+                        const uint32_t u = v % 3u;
+                        v /= 3u;
+                        dgt = u + (u >= xe[yy] ? 1u : 0u);
+                    }
+                    zb += dgt * Kn::wt(yy);
+                    o++;
+                }
+                rb[kF2Off[y] + i] = it < nsub * p3 * 8u ? zb * 64u + d8 : ~0u;
+            }
+        });
         constexpr bool TM = (PROBE & 16) != 0;
         uint64_t tm_vm = 0, tm_bar = 0, tm_rnd = 0, tm_end = 0, t0 = 0;
         const uint64_t tm_start = TM ? __builtin_amdgcn_s_memtime() : 0;
         for (uint32_t k = 0; k <= ntile; k++) {
-            for (int y = 0; y < 4; y++) {
+            sfor<4>([&](auto yc) BS_INL {
+                constexpr int y = decltype(yc)::value;
                 if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
                 if (k < ntile) {
                     // loads of step (k, y) landed; the loads issued after them may stay in flight
@@ -106,41 +148,19 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     t0 = t1;
                 }
                 if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
-                if (k == 0 || (PROBE & 1)) continue;
-                // ---- round of iscore level L = y + 1 of tile k - 1: every target layer z of level L
+                if (k == 0 || (PROBE & 1)) return;
+                // ---- round of iscore level y + 1 of tile k - 1: every target layer z of the level
                 // red in section Y adds sum over X != x_e(Y) of A_(Y,X) C(e_Y, z[Y := X]) (the three
-                // terms summed in registers, one 64-bit LDS atomic per row); targets enumerated
-                // arithmetically (z_Y = x_e(Y), L - 1 of the other sections red, base-3 digits for
-                // the rest)
-                const uint32_t L = uint32_t(y) + 1u;
-                const uint32_t nn = 4u - L, p3 = nn == 3u ? 27u : nn == 2u ? 9u : nn == 1u ? 3u : 1u;
-                const uint32_t nsub = (L == 1u || L == 4u) ? 1u : 3u;
-                for (uint32_t it = uint32_t(lane); it < nsub * p3 * 8u; it += 64u) {
-                    const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
-                    const uint32_t sub = ci / p3;
-                    uint32_t v = ci % p3;
-                    const uint32_t mask = L == 1u ? 0u : L == 2u ? (1u << sub) : L == 3u ? (7u ^ (4u >> sub)) : 7u;
-                    uint32_t zb = 0, o = 0;  // z without section Y's digit
+                // terms summed in registers, one 64-bit LDS atomic per row)
 #pragma unroll
-                    for (int yy = 0; yy < 4; yy++) {
-                        if (uint32_t(yy) == Y) continue;
-                        uint32_t dgt;
-                        if ((mask >> o) & 1u) {
-                            dgt = xe[yy];
-                        } else {
-                            const uint32_t u = v % 3u;
-                            v /= 3u;
-                            dgt = u + (u >= xe[yy] ? 1u : 0u);
-                        }
-                        zb += dgt * Kn::wt(yy);
-                        o++;
-                    }
-                    const uint32_t wy = Kn::wt(int(Y)), z = zb + xY * wy;
+                for (int i = 0; i < kF2Iters[y]; i++) {
+                    const uint32_t ob = rb[kF2Off[y] + i];
+                    if (ob == ~0u) continue;
                     uint32_t acc[4][2] = {};
 #pragma unroll
                     for (int j = 0; j < 3; j++) {
                         const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
-                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + (zb + X * wy) * 64u + d8);
+                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + ob + X * wy64);
                         const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
 #pragma unroll
                         for (int r = 0; r < 4; r++) {
@@ -148,14 +168,15 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                             acc[r][1] ^= gf_mul_idx(i1, tg[j][r]);
                         }
                     }
+                    const uint32_t oz = ob + xY * wy64;
 #pragma unroll
                     for (int r = 0; r < 4; r++)
-                        __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + z * 64u + d8),
+                        __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + oz),
                                                uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
-            }
+            });
             if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
             lds_barrier();  // B_r(k): every atomic of tile k-1 done (lgkmcnt(0) before the barrier)
             // the compute waves are past phase A(k): every ring buffer is free, so the next tile's
