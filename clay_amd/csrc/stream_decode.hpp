@@ -207,7 +207,8 @@ struct StreamDec {
     // section Y's alive nodes are loads qbase + sec_off[Y] .. of the ring (buffer = load % ring).
     // RT (k_stream_local): column digits at a.csh[y], and any number of erased nodes in section G
     // tbar (timing probe of k_stream_fused2 only): cycles spent in the four step barriers
-    template <int PROBE, bool RT = false>
+    // SB: a scheduling barrier after every node's fold (one node's values live at a time)
+    template <int PROBE, bool RT = false, bool SB = true>
     __device__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
                                    uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {  // R: ring depth
         sfor<4>([&](auto yc) BS_INL {
@@ -263,7 +264,7 @@ struct StreamDec {
                         transpose8(u);
                         fold<I, false>(u, S);
                     }
-                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
                 });
             } else {
                 // section G: all four nodes' slots are in the lane; U(a, g) = C(a, g) + gamma C(g, a)
@@ -292,7 +293,7 @@ struct StreamDec {
                         }
                         transpose8(v);
                         fold<4 * G + A, false>(v, S);
-                        __builtin_amdgcn_sched_barrier(0);
+                        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
                     });
                 } else if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
                     uint32_t v[8];
@@ -327,7 +328,7 @@ struct StreamDec {
                     });
                     transpose8(u);
                     fold<I, false>(u, S);
-                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
                 });
             }
         });

@@ -9,18 +9,19 @@
 //   * LDS = a ring of RB = 10 - ne node buffers (16 KiB: one node x 256 layers x 64 B) that
 //     streams continuously across tiles + a separate S/C region (ne x 16 KiB, [row r][z][64 B]);
 //   * 8 compute waves: phase A of tile k (StreamDec::phase_a, one barrier per section), the
-//     presolve S' = H_K^-1 S in registers (tables through scalar loads), then S'(k) into the S/C
-//     region once the region is free;
-//   * 4 loader waves issue every LDS-DMA (as in k_stream_syn) AND solve tile k-1 meanwhile: the
-//     round of iscore level y + 1 during section step y of tile k (term-parallel: one item per
-//     (target layer, section Y, node X) x 8 bytes, A_(Y,X) C(e_Y, z[Y:=X]) XORed into every C_r(z)
-//     with 64-bit LDS atomics; a wave owns one section Y: per target it sums the three X terms in
-//     registers (tables loaded once) and issues one atomic per row; a level's target layers are
-//     enumerated arithmetically -- no memory access but LDS);
-//   * after the last round the compute waves read C(k-1) into registers, hand the region over
-//     (S'(k) in) and store C(k-1): stores come from waves that never wait on vmcnt, so the
-//     loaders' counted DMA waits see loads only;
-//   * six workgroup barriers per tile (four section steps, rounds done, region free), all waves.
+//     presolve S' = H_K^-1 S in registers (check j outer: its row tables through scalar loads
+//     once per tile), then S'(k) into the S/C region (below);
+//   * 4 loader waves issue every LDS-DMA (as in k_stream_syn; the next tile's first loads once
+//     phase A freed the ring) AND solve tile k-1 meanwhile: the round of iscore level y + 1
+//     during section step y of tile k (term-parallel: one item per (target layer, 8 bytes); a
+//     wave owns one section Y and sums the three X != x_e(Y) terms A_(Y,X) C(e_Y, z[Y:=X]) of a
+//     target in registers (tables loaded once per kernel), one 64-bit LDS atomic XOR per row;
+//     every lane's target offsets are enumerated once per kernel and kept in registers);
+//   * after the last round each compute lane reads C(k-1) from, and writes S'(k) to, the same
+//     bytes of the region (no hand-over barrier), then stores C(k-1) (8-byte pieces, 64-byte row
+//     runs): stores come from waves that never wait on vmcnt, so the loaders' counted DMA waits
+//     see loads only;
+//   * five workgroup barriers per tile (four section steps, rounds done), all waves.
 // Tables live in global memory (scalar loads; the solver's in registers): the ring and the S/C
 // region take all 160 KiB of LDS.
 #pragma once
@@ -182,13 +183,12 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             // the compute waves are past phase A(k): every ring buffer is free, so the next tile's
             // first RB loads stream during the presolve, the region hand-over and the stores
             if (k + 1u < ntile) issue_upto((k + 1u) * NT + RB);
-            lds_barrier();  // B_w(k): the compute waves hold C(k-1); the region takes S'(k)
             if constexpr (TM) tm_end += __builtin_amdgcn_s_memtime() - t0;
         }
         wait_vm0();
         if constexpr (TM) {
             if (blockIdx.x == 0 && li == 0 && lane == 0)
-                printf("f2-timing loader tiles %u total %lu vmwait %lu barrier %lu rounds %lu br+bw %lu\n", ntile,
+                printf("f2-timing loader tiles %u total %lu vmwait %lu barrier %lu rounds %lu br %lu\n", ntile,
                        (unsigned long)(__builtin_amdgcn_s_memtime() - tm_start), (unsigned long)tm_vm,
                        (unsigned long)tm_bar, (unsigned long)tm_rnd, (unsigned long)tm_end);
         }
@@ -212,7 +212,8 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
-            Kn::template phase_a<(PROBE & 4) ? 2 : 0>(a, smem, k * NT, c0, poff0, xeG, S, RB, TM ? &tm_pabar : nullptr);
+            Kn::template phase_a<(PROBE & 4) ? 2 : 0, false, false>(a, smem, k * NT, c0, poff0, xeG, S, RB,
+                                                                    TM ? &tm_pabar : nullptr);
             // bit planes -> bytes
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -279,58 +280,50 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             tm_pre += t1 - t0;
             t0 = t1;
         }
-        // C(k-1) -> registers: 1,024 rows x 64 B, lane = one 16-byte piece of 16 rows per pass
-        uint4 ov[8];
-        if (k >= 1) {
+        // C(k-1) out of the region and S'(k) in: each lane reads, then overwrites, the same 16 x 8
+        // bytes (rows r, its four slots' layers, its 8-byte piece), so no lane can overwrite a
+        // byte another lane has yet to read -- no hand-over barrier
+        uint2 ov[16];  // [row r][slot g]
+        {
+            const uint32_t z0 = Kn::layer0(opq(c0));
 #pragma unroll
-            for (int i = 0; i < 8; i++)
-                if (uint32_t(i >> 1) < a.ne)  // rows of the region: ne (it holds ne x 16 KiB)
-                    ov[i] = *reinterpret_cast<const uint4 *>(scr + (uint32_t(i) * 512u + threadIdx.x) * 16u);
+            for (int r = 0; r < 4; r++) {
+                if (uint32_t(r) >= a.ne) continue;
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    uint2 *q = reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p);
+                    if (k >= 1) ov[r * 4 + g] = *q;
+                    if (k < ntile) *q = make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
+                }
+            }
         }
         if constexpr (TM) {
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
             tm_rd += t1 - t0;
             t0 = t1;
         }
-        lds_barrier();  // B_w(k): the region is free
-        if constexpr (TM) {
-            const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            tm_bw += t1 - t0;
-            t0 = t1;
-        }
-        if (k < ntile) {
-            const uint32_t z0 = Kn::layer0(opq(c0));
+        if (k >= 1 && !(PROBE & 2)) {
+            // 8-byte stores: eight lanes (p) write each layer's 64-byte row run of the tile
+            const typename Kn::Tile t = tm.tile(k - 1, wslot, ns);
+            if (t.b0 + 8u * p + 8u <= t.vend) {
+                const uint32_t z0 = Kn::layer0(opq(c0));
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-                if (uint32_t(r) < a.ne)
+                for (int r = 0; r < 4; r++) {
+                    uint8_t *dst = a.out[r];
+                    if (uint32_t(r) >= a.ne || !dst) continue;
 #pragma unroll
                     for (int g = 0; g < 4; g++)
-                        *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p) =
-                            make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
-        }
-        if (k >= 1 && !(PROBE & 2)) {
-            // piece i of this lane: row r = i / 2 (compile time), layer 128 (i & 1) + tid / 4,
-            // 16 bytes at 16 (tid & 3)
-            const typename Kn::Tile t = tm.tile(k - 1, wslot, ns);
-            const uint32_t pc = (threadIdx.x & 3u) * 16u, zl0 = threadIdx.x >> 2;
-            const bool full = t.b0 + pc + 16u <= t.vend, half = !full && t.b0 + pc + 8u <= t.vend;
-            const uint64_t off0 = uint64_t(zl0) * sc + t.b0 + pc;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const int r = i >> 1;
-                uint8_t *dst = a.out[r];
-                if (uint32_t(r) >= a.ne || !dst) continue;
-                uint8_t *o = dst + off0 + uint64_t(i & 1) * 128u * sc;
-                if (full) *reinterpret_cast<uint4 *>(o) = ov[i];
-                else if (half) *reinterpret_cast<uint2 *>(o) = make_uint2(ov[i].x, ov[i].y);
+                        *reinterpret_cast<uint2 *>(dst + uint64_t(z0 + uint32_t(g) * Kn::wt(G)) * sc + t.b0 + 8u * p) =
+                            ov[r * 4 + g];
+                }
             }
         }
         if constexpr (TM) tm_st += __builtin_amdgcn_s_memtime() - t0;
     }
     if constexpr (TM) {
         if (blockIdx.x == 0 && threadIdx.x == 0)
-            printf("f2-timing compute tiles %u total %lu phaseA %lu (barriers %lu) B_r %lu presolve %lu Cread %lu B_w %lu "
-                   "Swrite+stores %lu\n",
+            printf("f2-timing compute tiles %u total %lu phaseA %lu (barriers %lu) B_r %lu presolve %lu Cread+Swrite %lu - %lu "
+                   "stores %lu\n",
                    ntile, (unsigned long)(__builtin_amdgcn_s_memtime() - tm_start), (unsigned long)tm_pa,
                    (unsigned long)tm_pabar, (unsigned long)tm_br, (unsigned long)tm_pre, (unsigned long)tm_rd,
                    (unsigned long)tm_bw, (unsigned long)tm_st);
