@@ -121,7 +121,7 @@ def set_exec_mode(mode: str) -> str:
     eligible q = 4, t = 4 decode, else as auto), 'stream-fused' (as 'stream' on the fused
     single-launch decode kernel), 'stream-local' (the local decode for patterns with erasures
     in one y-section plus at most one other, which auto also runs), 'stream-fused2' (the fused
-    decode v2 for one erasure in every y-section, which auto also runs) or 'codeword' (as auto,
+    decode v2 for 2-4 erasures in distinct y-sections, which auto runs from 3 erasures) or 'codeword' (as auto,
     and a single erasure with every other chunk present in a q = m code is rebuilt by the repair
     kernel, reading 1/q of each chunk: the reference's bytes whenever the chunks are one
     codeword, NOT on arbitrary inputs).  Every other mode produces the reference's bytes on any

@@ -2057,7 +2057,7 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     bool ok = false;
     Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
     if (e || !ok) return e;
-    if (a.ne != 4) return Error{};  // one erasure in every section (the rounds' target enumeration)
+    if (a.ne < 2) return Error{};  // 2-4 erasures in distinct sections (the rounds' target enumeration)
     const uint32_t RB = 10 - a.ne;  // the S/C region takes ne of the 10 node buffers of LDS
     // the loads of a step are issued during the step before it (the ring holds both), also
     // across tiles: section 3 of tile k and section 0 of tile k + 1
@@ -2184,9 +2184,10 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     const bool autoish = xmode == kExecAuto || xmode == kExecCodeword;
     const bool try_local = autoish || xmode == kExecStreamLocal;
     const bool try_split = xmode == kExecStream || xmode == kExecStreamFused || (autoish && n_erased >= 3);
-    // fused decode v2 for one erasure in every section (the BASELINE {0,4,8,12}): auto and
-    // "stream-fused2" ((10,4,13) 1 GiB: 0.62 ms vs 0.74 split, profiles/r04/fused2/)
-    const bool try_f2 = xmode == kExecStreamFused2 || (autoish && n_erased == 4);
+    // fused decode v2 for 2-4 erasures in distinct sections: auto from 3 erasures and
+    // "stream-fused2" ((10,4,13) 1 GiB: {0,4,8,12} 0.52 ms vs 0.73 split, {0,4,8} 0.48 vs 0.62;
+    // {0,4} 0.458 vs 0.452 on the local decode; profiles/r04/fused2/)
+    const bool try_f2 = xmode == kExecStreamFused2 || (autoish && n_erased >= 3);
     if ((try_local || try_split || try_f2) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};

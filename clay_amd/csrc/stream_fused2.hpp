@@ -1,5 +1,5 @@
-// stream_fused2.hpp -- single-launch decode for q = 4, t = 4 codes with one erasure in each of the
-// four y-sections (the BASELINE worst case {0,4,8,12}): every survivor byte read from HBM
+// stream_fused2.hpp -- single-launch decode for q = 4, t = 4 codes with 2-4 erasures in distinct
+// y-sections (the BASELINE worst case {0,4,8,12} among them): every survivor byte read from HBM
 // once, every output byte written once, and the latency-bound iscore rounds (decode.rs:196-254)
 // of tile k-1 run on other waves while tile k streams.
 //
@@ -31,11 +31,12 @@
 namespace clay {
 namespace bs {
 
-// solver work items per lane and round: level 1 and 2 have 27 targets x 8 pieces (4 passes of 64
-// lanes), level 3 9 x 8 (2), level 4 1 x 8 (1)
-constexpr int kF2Iters[4] = {4, 4, 2, 1};
-constexpr int kF2Off[4] = {0, 4, 8, 10};
-constexpr int kF2Items = 11;
+// solver work items per lane and round (passes of 64 lanes over targets x 8 pieces), the most over
+// 2-4 erasures: level 1 has 27 / 36 / 48 targets for 4 / 3 / 2 erasures (4 / 5 / 6 passes),
+// level 2 27 / 24 / 16 (4 / 3 / 2), level 3 9 / 4 (2 / 1), level 4 1 (1)
+constexpr int kF2Iters[4] = {6, 4, 2, 1};
+constexpr int kF2Off[4] = {0, 6, 10, 12};
+constexpr int kF2Items = 13;
 
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
 // 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
@@ -72,57 +73,93 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         };
         issue_upto(RB);
-        // the rounds' work of this wave: the targets red in section Y = li (one wave per section);
-        // the A_(Y,X) tables of its three X != x_e(Y), loaded once into registers (tile-invariant)
-        uint32_t xe[4];
+        // the rounds' work of this wave: the targets red in section Y = li (one wave per section
+        // with an erasure; the wave of a section without one only loads); the A_(Y,X) tables of its
+        // three X != x_e(Y), loaded once into registers (tile-invariant; zero for an X outside the
+        // used shards: no dropped term, decode.rs:374)
+        const uint32_t ne = a.ne;
+        uint32_t xe[4], esec = 0;
 #pragma unroll
-        for (int y = 0; y < 4; y++) xe[y] = uint32_t(__builtin_ctz(a.emask[y]));
+        for (int y = 0; y < 4; y++) {
+            xe[y] = a.emask[y] ? uint32_t(__builtin_ctz(a.emask[y])) : 0u;
+            esec |= (a.emask[y] ? 1u : 0u) << y;
+        }
         const uint32_t Y = uint32_t(li), xY = xe[Y];
+        const bool wact = (esec >> Y) & 1u;
         GfTab tg[3][4];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
+            const bool use = wact && ((a.used >> (4u * Y + X)) & 1u);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                tg[j][r] = load_tab_c(tabc + (16u + (4u * Y + X) * 4u + uint32_t(r)) * 8u);
+                // loaded unconditionally (every table exists), then masked: zero = no term
+                const uint32_t keep = (use && uint32_t(r) < ne) ? ~0u : 0u;
+                const GfTab t = load_tab_c(tabc + (16u + (4u * Y + X) * 4u + uint32_t(r)) * 8u);
+                tg[j][r] = GfTab{t.w0 & keep, t.w1 & keep, t.w2 & keep, t.w3 & keep, t.w4 & keep};
                 asm volatile("" : "+v"(tg[j][r].w0), "+v"(tg[j][r].w1), "+v"(tg[j][r].w2), "+v"(tg[j][r].w3),
                              "+v"(tg[j][r].w4));
             }
         }
-        const uint8_t *src = scr + uint32_t(a.rix[4u * Y + xY]) * BUF;  // C(e_Y, .)
+        // C(e_Y, .): rix read unconditionally (xY = 0 for a section without an erasure), then the
+        // value selected -- a select between loads would become a load through a selected pointer
+        // and move the kernel arguments to scratch memory
+        const uint32_t rY = opq(uint32_t(a.rix[4u * Y + xY]));
+        const uint8_t *src = scr + (wact ? rY : 0u) * BUF;
         const uint32_t wy64 = Kn::wt(int(Y)) * 64u;
         // the lane's work items of every round, tile-invariant: byte offset (layer without section
         // Y's digit) x 64 + 8-byte piece, ~0 = none.  Level L's targets: z_Y = x_e(Y), L - 1 of the
-        // other sections red (sub-set `sub` of the C(3, L - 1)), base-3 digits for the rest.
+        // other erased sections red (subset `sub`), base-3 digits for the other erased sections,
+        // base-4 digits for the sections without an erasure; the lowest-weight section's digit
+        // varies fastest (neighbouring items on different LDS banks)
         uint32_t rb[kF2Items];
+        const uint32_t no = uint32_t(__builtin_popcount(esec)) - (wact ? 1u : 0u);  // other erased sections
+        const uint32_t n4 = 4u - uint32_t(__builtin_popcount(esec));                // sections without one
         sfor<4>([&](auto yc) BS_INL {
             constexpr int y = decltype(yc)::value;
-            constexpr uint32_t L = uint32_t(y) + 1u, nn = 4u - L;
-            constexpr uint32_t p3 = nn == 3u ? 27u : nn == 2u ? 9u : nn == 1u ? 3u : 1u;
-            constexpr uint32_t nsub = (L == 1u || L == 4u) ? 1u : 3u;
+            constexpr uint32_t L = uint32_t(y) + 1u;
+            uint32_t c3 = 1, c4 = 1, nsub = 0;
+            for (uint32_t i = 0; i + (L - 1u) < no; i++) c3 *= 3u;
+            for (uint32_t i = 0; i < n4; i++) c4 *= 4u;
+            for (uint32_t m = 0; m < (1u << no); m++) nsub += uint32_t(__builtin_popcount(m)) == L - 1u ? 1u : 0u;
+            const uint32_t per = c3 * c4, total = (wact && L - 1u <= no) ? nsub * per : 0u;
 #pragma unroll
             for (int i = 0; i < kF2Iters[y]; i++) {
                 const uint32_t it = uint32_t(lane) + 64u * uint32_t(i);
                 const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
-                const uint32_t sub = ci / p3;
-                uint32_t v = ci % p3;
-                const uint32_t mask = L == 1u ? 0u : L == 2u ? (1u << sub) : L == 3u ? (7u ^ (4u >> sub)) : 7u;
-                uint32_t zb = 0, o = 0;
-#pragma unroll
-                for (int yy = 0; yy < 4; yy++) {
-                    if (uint32_t(yy) == Y) continue;
+                if (ci >= total) {
+                    rb[kF2Off[y] + i] = ~0u;
+                    continue;
+                }
+                const uint32_t sub = ci / per;
+                uint32_t v = ci % per, mask = 0, cnt = 0;
+                for (uint32_t m = 0; m < (1u << no); m++)
+                    if (uint32_t(__builtin_popcount(m)) == L - 1u) {
+                        if (cnt == sub) mask = m;
+                        cnt++;
+                    }
+                uint32_t zb = 0, o = 0;  // o: index among the other erased sections (descending)
+                sfor<4>([&](auto qc) BS_INL {
+                    constexpr int yy = 3 - decltype(qc)::value;
+                    if (uint32_t(yy) == Y) return;
+                    const uint32_t xy = xe[yy];
                     uint32_t dgt;
-                    if ((mask >> o) & 1u) {
-                        dgt = xe[yy];
+                    if ((esec >> yy) & 1u) {
+                        if ((mask >> o) & 1u) {
+                            dgt = xy;
+                        } else {
+                            const uint32_t u = v % 3u;
+                            v /= 3u;
+                            dgt = u + (u >= xy ? 1u : 0u);
+                        }
+                        o++;
                     } else {
-                        const uint32_t u = v % 3u;
-                        v /= 3u;
-                        dgt = u + (u >= xe[yy] ? 1u : 0u);
+                        dgt = v & 3u;
+                        v >>= 2;
                     }
                     zb += dgt * Kn::wt(yy);
-                    o++;
-                }
-                rb[kF2Off[y] + i] = it < nsub * p3 * 8u ? zb * 64u + d8 : ~0u;
+                });
+                rb[kF2Off[y] + i] = zb * 64u + d8;
             }
         });
         constexpr bool TM = (PROBE & 16) != 0;
@@ -172,9 +209,10 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     const uint32_t oz = ob + xY * wy64;
 #pragma unroll
                     for (int r = 0; r < 4; r++)
-                        __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + oz),
-                                               uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (uint32_t(r) < ne)  // the region holds ne rows
+                            __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + oz),
+                                                   uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
             });

@@ -273,8 +273,9 @@ int clay_set_encode_path(int mode);
  *                per-level executor; decodes of >= 3 erasures of q = 4, t = 4 codes
  *                ((10,4,13), (9,4,12)) in distinct y-sections with sc % 8 == 0, sc >= 512 run
  *                the split streaming decode (k_stream_syn + k_stream_solve, last path
- *                "stream-split") -- with one erasure in every section (the BASELINE
- *                {0,4,8,12}) the fused decode v2 instead (k_stream_fused2, "stream-fused2");
+ *                "stream-split") -- when the ring fits (every 3- and 4-erasure pattern of
+ *                (10,4,13), the BASELINE {0,4,8,12} included) the fused decode v2 instead
+ *                (k_stream_fused2, "stream-fused2");
  *                decodes of those codes whose erasures lie in one y-section
  *                plus at most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4},
  *                {0,1,2,3}, ...) run the single-launch local decode (k_stream_local,
@@ -289,9 +290,9 @@ int clay_set_encode_path(int mode);
  *                streaming decode ("stream-split"); everything else as auto
  *   4 stream-fused -- as stream, but on the fused single-launch k_stream_decode ("stream")
  *   5 stream-local -- every decode the local kernel takes on it ("stream-local"); else as auto
- *   6 stream-fused2 -- decodes with one erasure in each y-section on the fused decode v2
- *                (k_stream_fused2, "stream-fused2"; ring of 6 node buffers: any two
- *                neighbouring sections hold <= 6 surviving real nodes); else as auto
+ *   6 stream-fused2 -- decodes of 2-4 erasures in distinct y-sections on the fused decode v2
+ *                (k_stream_fused2, "stream-fused2"; ring of 10 - e node buffers: any two
+ *                neighbouring sections hold <= 10 - e surviving real nodes); else as auto
  *   7 codeword -- as auto, for callers whose chunks are one codeword (the crate's usage: chunks
  *                it encoded): a decode of ONE erased node with every other node present, in a
  *                q = m code ((9,3,11), (10,4,13)), is rebuilt by k_bs_repair_stream from the whole

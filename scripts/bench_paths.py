@@ -146,6 +146,13 @@ if __name__ == "__main__":
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
             ("split", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "stream")),
             ("split", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "stream-fused2")),
+            # the fused decode v2 for 3 and 2 erasures in distinct sections (auto: split / local)
+            ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8], "stream-fused2")),
+            ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),
+            ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [1, 9, 13], "stream-fused2")),
+            ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [1, 9, 13])),
+            ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4], "stream-fused2")),
+            ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0])),
             ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
             ("decode23", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),

@@ -130,9 +130,9 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, auto_exe
 
 
 def fused2_eligible(c, er):
-    """k_stream_fused2: one erasure in every y-section and a ring of 10 - e node buffers that
+    """k_stream_fused2: 2-4 erasures in distinct y-sections and a ring of 10 - e node buffers that
     holds any two neighbouring sections' surviving real nodes."""
-    if not stream_eligible(c, er) or len(er) != c.t:
+    if not stream_eligible(c, er) or not 2 <= len(er) <= c.t:
         return False
     alive = [0] * c.t
     for i in range(c.n):
@@ -145,15 +145,20 @@ def fused2_eligible(c, er):
 @pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
 @pytest.mark.parametrize("sc", [512, 520, 64 * 37 + 40])
 def test_fused2_decode_random_inputs(oracle_mod, torch_cuda, cfg, sc):
-    """Exec mode "stream-fused2" (stream_fused2.hpp): a sample of the eligible 4-erasure patterns
-    (one per section) on random chunks, erased data chunks bit-exact vs the oracle."""
+    """Exec mode "stream-fused2" (stream_fused2.hpp): samples of the eligible 4-, 3- and 2-erasure
+    patterns (distinct sections; the unused survivor of a 2- or 3-erasure pattern may share a
+    section with an erasure) on random chunks, erased data chunks bit-exact vs the oracle."""
     torch = torch_cuda
     c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
     chunk = c.sub_chunk_no * sc
     rng = np.random.default_rng(sc + 3 * cfg[0])
-    pats = [list(e) for e in itertools.combinations(range(c.n), 4) if fused2_eligible(c, list(e))]
-    pats = [pats[i] for i in rng.permutation(len(pats))[:40]]
+    pats = []
+    for r, cnt in ((4, 30), (3, 20), (2, 10)):
+        allp = [list(e) for e in itertools.combinations(range(c.n), r) if fused2_eligible(c, list(e))]
+        pats += [allp[i] for i in rng.permutation(len(allp))[:cnt]]
     pats.insert(0, [0, 4, 8, 12] if cfg == (10, 4, 13) else [0, 4, 8, 11])
+    pats.insert(1, [0, 4, 8])
+    pats.insert(2, [4, c.n - 1])
     prev = clay_amd.set_exec_mode("stream-fused2")
     try:
         for er in pats:
@@ -170,25 +175,27 @@ def test_fused2_decode_random_inputs(oracle_mod, torch_cuda, cfg, sc):
 
 @pytest.mark.parametrize("sc", [520, 64 * 8 * 33 + 24])
 def test_fused2_decode_codeword_incl_parity_and_grouped(oracle_mod, torch_cuda, sc):
-    """The BASELINE worst case {0,4,8,12} on a codeword (every rebuilt chunk incl. parity node 12)
-    and on random inputs against the grouped plan executor (parity outputs included)."""
+    """The BASELINE worst case {0,4,8,12} and 3- / 2-erasure patterns with parity nodes on a
+    codeword (every rebuilt chunk incl. parity) and on random inputs against the grouped plan
+    executor (parity outputs included)."""
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     chunk = c.sub_chunk_no * sc
-    er = [0, 4, 8, 12]
     ref = o.encode_array(np.random.default_rng(sc).integers(0, 256, c.k * chunk, dtype=np.uint8))
     prev = clay_amd.set_exec_mode("stream-fused2")
     try:
-        got = _decode_dev(torch, c, ref, er, chunk)
-        assert clay_amd.last_exec_path() == "stream-fused2"
-        for e in er:
-            assert np.array_equal(got[e], ref[e]), e
-        chunks = np.random.default_rng(sc + 1).integers(0, 256, (c.n, chunk), dtype=np.uint8)
-        a = _decode_dev(torch, c, chunks, er, chunk)
-        clay_amd.set_exec_mode("grouped")
-        b = _decode_dev(torch, c, chunks, er, chunk)
-        assert clay_amd.last_exec_path() == "grouped"
-        for e in er:
-            assert np.array_equal(a[e], b[e]), e
+        for er in ([0, 4, 8, 12], [0, 4, 8], [1, 9, 13], [5, 12]):
+            clay_amd.set_exec_mode("stream-fused2")
+            got = _decode_dev(torch, c, ref, er, chunk)
+            assert clay_amd.last_exec_path() == "stream-fused2", er
+            for e in er:
+                assert np.array_equal(got[e], ref[e]), (er, e)
+            chunks = np.random.default_rng(sc + len(er)).integers(0, 256, (c.n, chunk), dtype=np.uint8)
+            a = _decode_dev(torch, c, chunks, er, chunk)
+            clay_amd.set_exec_mode("grouped")
+            b = _decode_dev(torch, c, chunks, er, chunk)
+            assert clay_amd.last_exec_path() == "grouped"
+            for e in er:
+                assert np.array_equal(a[e], b[e]), (er, e)
     finally:
         clay_amd.set_exec_mode(prev)
