@@ -62,8 +62,11 @@ def parse(argv=None):
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-small", action="store_true", help="skip the clay_bench-size GPU batch rates")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the driver-timed legs of BASELINE configs 2, 3 and 5 (after the timed region)")
+    ap.add_argument("--leg-calls", type=int, default=20, help="timed calls per config leg")
     ap.add_argument("--path", default="auto",
-                    choices=["auto", "fused", "staged", "bitsliced", "bitsliced6", "stream"])
+                    choices=["auto", "fused", "staged", "bitsliced", "stream"])
     ap.add_argument("--tile", type=int, default=0, help="encode path variant (clay_set_encode_path)")
     ap.add_argument("--launch-timeout", type=float, default=900.0,
                     help="--gpus N launcher: stop every rank after this many seconds (0 = no limit)")
@@ -289,6 +292,133 @@ def small_stripe_rates(torch, dev, local, sh):
     return out
 
 
+def _event_times(torch, stream, fn, calls: int, warm: int = 3):
+    """HIP-event time of each of `calls` back-to-back calls on `stream` (events recorded on the
+    launch stream, all calls queued before one synchronize), after `warm` untimed calls."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(calls)]
+    for a, b in evs:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in evs]
+
+
+def _leg(name, ms, algo, path, verified, extra=None):
+    mean = float(np.mean(ms))
+    d = {"workload": name, "kernel_ms_mean": round(mean, 4), "kernel_ms_min": round(float(min(ms)), 4),
+         "calls": len(ms), "algorithmic_bytes": int(algo), "achieved_GBps": round(algo / (mean * 1e-3) / 1e9, 1),
+         "frac": round(algo / (mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "path": path, "verified_vs_oracle": verified}
+    if extra:
+        d.update(extra)
+    return d
+
+
+def _slice_cols(arr2d, alpha, p0, w):
+    """Columns [p0, p0 + w) of every sub-chunk of each row of a (rows, alpha * sc) device tensor,
+    as a host array (rows, alpha * w): an independent smaller instance of the same code."""
+    rows = arr2d.shape[0]
+    sc = arr2d.shape[1] // alpha
+    return arr2d.view(rows, alpha, sc)[:, :, p0:p0 + w].contiguous().cpu().numpy().reshape(rows, alpha * w)
+
+
+def config_legs(torch, dev, local, stream, oracle_cls, calls: int):
+    """Driver-timed legs for the other BASELINE GPU configs,
+    each run AFTER the encode's timed region on fresh device buffers: HIP-event kernel time per
+    call, the §8(d) algorithmic bytes, the fraction of 8 TB/s, the kernel path, and a column-slice
+    check against the oracle (every byte offset of the sub-chunks is an independent codeword, so
+    positions [p0, p0 + w) of every sub-chunk form a small instance of the same call)."""
+    import clay_amd
+    from clay_amd import ClayCode
+    sh = stream.cuda_stream
+    out = {}
+    g = torch.Generator(device=dev)
+
+    def rnd(shape, seed):
+        g.manual_seed(seed)
+        return torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=g)
+
+    # config 5: (10,4,13) 1 GiB stripe, 4 erasures {0,4,8,12} (worst case), random chunks
+    c = ClayCode(10, 4, 13)
+    chunk = c.encoded_chunk_size(1 << 30)
+    alpha, sc = c.sub_chunk_no, chunk // c.sub_chunk_no
+    er = [0, 4, 8, 12]
+    full = rnd((c.n, chunk), 51)
+    outs = torch.zeros((c.n, chunk), dtype=torch.uint8, device=dev)
+    ins = [None if i in er else full[i] for i in range(c.n)]
+    ous = [outs[i] if i in er else None for i in range(c.n)]
+    ms = _event_times(torch, stream, lambda: c.decode_device(ins, er, ous, chunk, local, sh), calls)
+    path = clay_amd.last_exec_path()
+    o = oracle_cls(10, 4, 13)
+    ok = True
+    for p0 in (0, sc - VERIFY_W):
+        s = _slice_cols(full, alpha, p0, VERIFY_W)
+        got = _slice_cols(outs, alpha, p0, VERIFY_W)
+        ref = np.frombuffer(o.decode({i: s[i] for i in range(c.n) if i not in er}, er), np.uint8).reshape(10, -1)
+        ok = ok and all(np.array_equal(got[e], ref[e]) for e in er if e < 10)
+    algo = (c.n - len(er)) * chunk + sum(1 for e in er if e < 10) * chunk
+    out["decode_cfg5"] = _leg("(k=10,m=4,d=13) decode, 1 GiB stripe, erasures {0,4,8,12}, random chunks",
+                              ms, algo, path, ok, {"bytes_counted": "10 survivors read + 3 erased data chunks written"})
+    del full, outs, ins, ous
+
+    # config 3: (9,3,11) repair of node 0 from d = 11 helpers, chunk 268,435,458 (beta sub-chunks each)
+    c = ClayCode(9, 3, 11)
+    chunk = 268_435_458
+    alpha, sc = c.sub_chunk_no, chunk // c.sub_chunk_no
+    info = c.minimum_to_repair(0, [i for i in range(c.n) if i != 0])
+    helpers, idx = [h for h, _ in info], info[0][1]
+    beta = len(idx)
+    hb = rnd((len(helpers), beta * sc), 31)
+    rep = torch.zeros(chunk, dtype=torch.uint8, device=dev)
+    hl = [hb[i] for i in range(len(helpers))]
+    ms = _event_times(torch, stream, lambda: c.repair_device(0, helpers, hl, chunk, rep, local, sh), calls)
+    path = clay_amd.last_exec_path()
+    o = oracle_cls(9, 3, 11)
+    ok = True
+    for p0 in (0, sc - VERIFY_W):
+        hs = _slice_cols(hb, beta, p0, VERIFY_W)
+        got = _slice_cols(rep.view(1, -1), alpha, p0, VERIFY_W)[0]
+        ref = o.repair(0, {h: hs[j] for j, h in enumerate(helpers)}, alpha * VERIFY_W)
+        ok = ok and np.array_equal(got, np.frombuffer(ref, np.uint8))
+    algo = len(helpers) * beta * sc + chunk
+    out["repair_cfg3"] = _leg("(k=9,m=3,d=11) repair of node 0 from 11 helpers, chunk 268,435,458",
+                              ms, algo, path, ok, {"bytes_counted": "d x beta x sc read + the chunk written"})
+    del hb, rep, hl
+
+    # config 2: (4,2,5) 64 MiB stripe: encode, then decode of erasure {0}
+    c = ClayCode(4, 2, 5)
+    chunk = c.encoded_chunk_size(64 << 20)
+    alpha, sc = c.sub_chunk_no, chunk // c.sub_chunk_no
+    full = torch.zeros((c.n, chunk), dtype=torch.uint8, device=dev)
+    full[:4] = rnd((4, chunk), 21)
+    dl, pl = [full[i] for i in range(4)], [full[4 + i] for i in range(2)]
+    ms_e = _event_times(torch, stream, lambda: c.encode_device(dl, pl, chunk, local, sh), calls)
+    epath = clay_amd.last_encode_path()
+    o = oracle_cls(4, 2, 5)
+    ok_e = True
+    for p0 in (0, sc - VERIFY_W):
+        s = _slice_cols(full, alpha, p0, VERIFY_W)
+        ok_e = ok_e and np.array_equal(s[4:], o.encode_array(s[:4].reshape(-1))[4:])
+    outs = torch.zeros((c.n, chunk), dtype=torch.uint8, device=dev)
+    er = [0]
+    ins = [None if i in er else full[i] for i in range(c.n)]
+    ous = [outs[i] if i in er else None for i in range(c.n)]
+    ms_d = _event_times(torch, stream, lambda: c.decode_device(ins, er, ous, chunk, local, sh), calls)
+    dpath = clay_amd.last_exec_path()
+    ok_d = bool(torch.equal(outs[0], full[0]))  # a codeword: the erased chunk comes back exactly
+    out["cfg2_encode"] = _leg("(k=4,m=2,d=5) encode, 64 MiB stripe", ms_e, 6 * chunk, epath, ok_e,
+                              {"bytes_counted": "4 data chunks read + 2 parity written"})
+    out["cfg2_decode"] = _leg("(k=4,m=2,d=5) decode of erasure {0}, 64 MiB stripe (a codeword)", ms_d,
+                              5 * chunk + chunk, dpath, ok_d,
+                              {"bytes_counted": "5 survivors read + 1 erased data chunk written"})
+    del full, outs, ins, ous
+    torch.cuda.synchronize()
+    return out
+
+
 def latest_traffic():
     """Per-launch HBM bytes from the newest committed PMC summary (profiles/*encode*_pmc.json)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*encode*_pmc.json")))
@@ -404,7 +534,7 @@ def run_rank(args) -> int:
         per = [mine.cpu().tolist()]
     tmax = max(p[0] for p in per)
 
-    host_incl = host_sync = small = None
+    host_incl = host_sync = small = legs = None
     if rank == 0 and world == 1 and not args.cpu_dry:
         if not args.no_host_path:
             # PCIe-inclusive: pinned host data chunks -> device -> parity back to
@@ -432,6 +562,9 @@ def run_rank(args) -> int:
                 verified = verified and bool(torch.equal(hdst, par.cpu()))
         if not args.no_small:
             small = small_stripe_rates(torch, dev_t, local, sh)
+        if not args.no_legs:
+            del data, par, dptr, pptr
+            legs = config_legs(torch, dev_t, local, stream, oracle.OracleClay, args.leg_calls)
 
     if rank != 0:
         if world > 1:
@@ -475,6 +608,7 @@ def run_rank(args) -> int:
         "host_inclusive_GiBps": host_incl,
         "host_inclusive_sync_GiBps": host_sync,
         "gpu_small_stripes": small,
+        "config_legs": legs,
     }
     if args.cpu_dry:
         out["cpu_dry"] = True

@@ -90,15 +90,15 @@ def _ptr(x) -> int:
     return int(x)
 
 
-_ENCODE_PATHS = {"auto": 0, "staged": 1, "fused": 2, "bitsliced": 3, "bitsliced6": 4, "stream": 5}
+_ENCODE_PATHS = {"auto": 0, "staged": 1, "fused": 2, "bitsliced": 3, "stream": 5}
 
 
 def set_encode_path(mode: str, tile: int = 0) -> str:
-    """Process-wide encode path: 'auto' | 'staged' | 'fused' | 'bitsliced' | 'bitsliced6' | 'stream'.
+    """Process-wide encode path: 'auto' | 'staged' | 'fused' | 'bitsliced' | 'stream'.
 
-    `tile` selects a variant: 'bitsliced' lanes per column group (0, 1, 4), 'bitsliced6'
-    tile width (0 = 256 B, 4 = 128 B), 'stream' loader waves for (10,4,13) (0 = default 4, 1, 2, 4;
-    (9,4,12) always runs 4). Only 'stream' and 'bitsliced6' need 8-byte rows (sc % 8 == 0).
+    `tile` selects a variant: 'bitsliced' lanes per column group (0, 1, 4), 'stream' loader
+    waves for (10,4,13) (0 = default 4, 1, 2, 4; (9,4,12) always runs 4; (9,3,11) 2, or 7 for
+    variant 7). 'stream' (10,4,13) / (9,4,12) needs 8-byte rows (sc % 8 == 0).
     Every accepted path produces the reference's parity; anything else raises ValueError.
     Returns the previous path name."""
     if mode not in _ENCODE_PATHS:
@@ -109,23 +109,18 @@ def set_encode_path(mode: str, tile: int = 0) -> str:
     return {v: k for k, v in _ENCODE_PATHS.items()}.get(prev & 0xFF, "auto")
 
 
-_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-fused": 4, "stream-local": 5, "stream-fused2": 6,
-               "codeword": 7}
+_EXEC_MODES = {"auto": 0, "grouped": 1, "tile": 2, "stream": 3, "stream-local": 5, "stream-fused2": 6}
 
 
 def set_exec_mode(mode: str) -> str:
-    """Process-wide plan executor for decode / repair / staged encode: 'auto' (tile-fused
-    where the U slots fit in LDS, else grouped; the split streaming decode for >= 3 erasures of
-    q = 4, t = 4 codes; the bit-sliced repair kernels for q = m repairs from all n - 1 nodes),
-    'grouped' (one launch per level), 'tile', 'stream' (the split streaming decode for every
-    eligible q = 4, t = 4 decode, else as auto), 'stream-fused' (as 'stream' on the fused
-    single-launch decode kernel), 'stream-local' (the local decode for patterns with erasures
-    in one y-section plus at most one other, which auto also runs), 'stream-fused2' (the fused
-    decode v2 for 2-4 erasures in distinct y-sections, which auto runs from 3 erasures) or 'codeword' (as auto,
-    and a single erasure with every other chunk present in a q = m code is rebuilt by the repair
-    kernel, reading 1/q of each chunk: the reference's bytes whenever the chunks are one
-    codeword, NOT on arbitrary inputs).  Every other mode produces the reference's bytes on any
-    input.  Returns the previous mode."""
+    """Process-wide plan executor for decode / repair / staged encode (clay.h): 'auto' (tile-fused
+    where the U slots fit in LDS, else grouped; for q = 4, t = 4 codes the local decode for
+    erasures in one y-section plus at most one other, the fused decode v2 for 3-4 erasures in
+    distinct y-sections; the bit-sliced repair kernels for q = m repairs from all n - 1 nodes),
+    'grouped' (one launch per level), 'tile', 'stream' (every decode a streaming kernel takes:
+    local, else fused v2 from 2 erasures; the streaming repair kernel at any sub-chunk size),
+    'stream-local' or 'stream-fused2' (that kernel wherever it applies).  Modes choose kernels
+    only: every mode returns the reference's bytes on any input.  Returns the previous mode."""
     if mode not in _EXEC_MODES:
         raise ValueError(f"unknown exec mode {mode!r}")
     prev = _lib.lib().clay_set_exec_mode(_EXEC_MODES[mode])
@@ -134,7 +129,7 @@ def set_exec_mode(mode: str) -> str:
 
 def last_exec_path() -> str:
     """Plan executor of this thread's last decode / repair / staged encode: 'tile' | 'grouped' |
-    'stream-split' | 'stream' | 'bs-repair-stream' | 'bs-repair' | 'none'."""
+    'stream-local' | 'stream-fused2' | 'bs-repair-stream' | 'bs-repair' | 'none'."""
     return _lib.lib().clay_last_exec_path().decode()
 
 
@@ -148,7 +143,8 @@ def release_workspace(device: int = 0) -> None:
 
 def release_captured(device: int = 0) -> None:
     """Reclaim the pointer-table arena and the pooled workspaces that calls inside stream
-    captures left to their graphs; call once those graphs are destroyed (clay.h)."""
+    captures left to their graphs; call once every replay of those graphs has completed and the
+    graphs are destroyed (clay.h: no device-wide synchronize is taken)."""
     err = ClayErrorStruct()
     rc = _lib.lib().clay_release_captured(int(device), C.byref(err))
     if rc:
@@ -353,15 +349,18 @@ class ClayCode:
             _raise(rc, err)
 
     def decode_device(self, chunks, erasures: Sequence[int], out_chunks, chunk_size: int,
-                      device: int = 0, stream: int = 0):
-        """chunks / out_chunks: n entries, None where absent (see clay.h)."""
+                      device: int = 0, stream: int = 0, codeword: bool = False):
+        """chunks / out_chunks: n entries, None where absent (see clay.h).  codeword=True calls
+        clay_decode_device_codeword: the caller vouches that the chunks are one codeword, so a
+        single erasure may be rebuilt by the repair kernel (1/q of every chunk read); for this
+        call only."""
         cp = (C.c_void_p * self.n)(*[(_ptr(x) if x is not None else None) for x in chunks])
         op = (C.c_void_p * self.n)(*[(_ptr(x) if x is not None else None) for x in out_chunks])
         er = list(erasures)
         err = ClayErrorStruct()
-        rc = _lib.lib().clay_decode_device(C.byref(self._c), cp, _sizes(er), len(er), op,
-                                           int(chunk_size), int(device), C.c_void_p(int(stream)),
-                                           C.byref(err))
+        fn = _lib.lib().clay_decode_device_codeword if codeword else _lib.lib().clay_decode_device
+        rc = fn(C.byref(self._c), cp, _sizes(er), len(er), op, int(chunk_size), int(device),
+                C.c_void_p(int(stream)), C.byref(err))
         if rc:
             _raise(rc, err)
 

@@ -48,6 +48,8 @@ SIGNATURES = {
                                              _err_p]),
     "clay_decode_device": (C.c_int, [_code_p, _P(_vp), _P(_sz), _sz, _P(_vp), _sz, C.c_int, _vp,
                                      _err_p]),
+    "clay_decode_device_codeword": (C.c_int, [_code_p, _P(_vp), _P(_sz), _sz, _P(_vp), _sz, C.c_int, _vp,
+                                              _err_p]),
     "clay_repair_device": (C.c_int, [_code_p, _sz, _P(_sz), _P(_vp), _sz, _sz, _vp, C.c_int, _vp,
                                      _err_p]),
     "clay_repair_device_full_chunks": (C.c_int, [_code_p, _sz, _P(_sz), _P(_vp), _sz, _sz, _vp,

@@ -22,18 +22,10 @@ struct DecArgs {
     uint32_t nt;              // loads per tile (alive nodes)
     uint32_t sec_off[5];      // first load of section y's step within a tile
     uint32_t load_node[16];   // internal node of each load of a tile
-    uint32_t nround;          // phase-B rounds
-    uint32_t round1;          // first round of iscore level >= 1 (split solve: level 0 is C = S')
-    uint32_t pstart[25];      // split solve: correction pairs of round r at [pstart[r], pstart[r+1])
-    uint32_t round_start[24]; // first entry of each round in the layer order (+ end)
-    // device buffer (kDecTabWords dwords), copied into LDS for phase B: v_perm tables of 8
-    // dwords each (5 used) -- table t = r * 4 + j: row e_r of H_K^-1, check j; table
-    // 16 + i * 4 + r: A_i[e_r] = (H_K^-1 gamma H_i)[e_r] for node i; then the phase-B layer
-    // order (256 bytes) at dword kDecOrder
+    // device buffer (kDecTabWords dwords) of v_perm tables, 8 dwords each (5 used): table
+    // t = r * 4 + j: row e_r of H_K^-1, check j; table 16 + i * 4 + r: A_i[e_r] =
+    // (H_K^-1 gamma H_i)[e_r] for node i; table kDecDetInv: det^-1 (local decode only)
     const uint32_t *tabs;
-    // split mode (k_stream_syn + k_stream_solve): S of tile b0 / 64 at ws + (b0 / 64) * 64 KiB,
-    // layout [check j][layer z][64 B] (the S/C region of the fused kernel)
-    uint8_t *ws;
     // local decode (k_stream_local): bit position of section y's layer digit in the column c
     // (a permutation of 0, 2, 4 over the sections != G; section g2's digit at 0, so its lines
     // are lanes l, l ^ 8, l ^ 16, l ^ 24 of one wave); g2 = the section of the one erasure
@@ -44,12 +36,9 @@ struct DecArgs {
 };
 // local decode: v_perm table of det^-1 = (1 + gamma^2)^-1 (pair inversion, transforms.rs:108-125)
 constexpr int kDecDetInv = 80;
-constexpr int kDecOrder = 640;
-// split solve: correction pairs (uint16 layer | Y << 8 | X << 10: C(e_Y, z[Y:=X]) feeds layer z)
-// from dword kDecPairs; at most 768 (4 erasures: 108 x 3 + 54 x 6 + 12 x 9 + 12)
-constexpr int kDecPairs = 704;
-constexpr int kDecMaxPairs = 1152;
-constexpr int kDecTabWords = 1280;  // 5 KiB: 1 KiB LDS-DMA instructions (the fused kernel copies the first 3)
+// 3 KiB: k_stream_local copies them into LDS with three 1 KiB LDS-DMA instructions
+constexpr int kDecTabWords = 768;
+static_assert((kDecDetInv + 1) * 8 <= kDecTabWords, "every table inside the block the kernels copy");
 
 }  // namespace bs
 }  // namespace clay

@@ -31,7 +31,6 @@
 #include "code.hpp"
 #include "gf256.hpp"
 #include "bitslice.hpp"
-#include "bitslice6.hpp"
 #include "stream_encode.hpp"
 #include "repair_args.hpp"  // bit-sliced repair kernel: repair_kernel.hpp, instantiated in repair_stream.hip
 #include "decode_args.hpp"  // streaming-decode kernel: stream_decode.hpp, instantiated in decode_stream.hip
@@ -541,8 +540,9 @@ __global__ __launch_bounds__(kFusedBlock) void k_fused_encode(FusedArgs a, const
 static thread_local std::string t_last_path = "none";
 static thread_local size_t t_last_launches = 0;
 static thread_local const char *t_last_exec = "none";  // plan executor of the last run_plan
-// Encode path selection (clay_set_encode_path): process-wide, read without locks.
-enum : int { kModeAuto = 0, kModeStaged = 1, kModeFused = 2, kModeBs = 3, kModeBs6 = 4, kModeStream = 5 };
+// Encode path selection (clay_set_encode_path): process-wide, read without locks (4 was the
+// retired v6 kernel, now unused).
+enum : int { kModeAuto = 0, kModeStaged = 1, kModeFused = 2, kModeBs = 3, kModeStream = 5 };
 static std::atomic<int> g_encode_mode{kModeAuto};
 static std::atomic<int> g_encode_tile{0};  // per-mode variant (see clay_set_encode_path)
 
@@ -1098,8 +1098,10 @@ static int align_of(uintptr_t p) {
 }
 
 // Executor selection (clay_set_exec_mode): process-wide, read without locks.
-enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3, kExecStreamFused = 4,
-              kExecStreamLocal = 5, kExecStreamFused2 = 6, kExecCodeword = 7 };  // see clay_set_exec_mode
+// Modes only choose kernels: every mode returns the reference's bytes on any input (4, the
+// retired single-launch decode, and 7, now the per-call clay_decode_device_codeword, are unused).
+enum : int { kExecAuto = 0, kExecGrouped = 1, kExecTile = 2, kExecStream = 3, kExecStreamLocal = 5,
+              kExecStreamFused2 = 6 };  // see clay_set_exec_mode
 static std::atomic<int> g_exec_mode{kExecAuto};
 static size_t tex_lds_budget() { return tuning().texec_lds; }
 // Lane width of the tile-fused executor for a plan (0 = not eligible): the widest of
@@ -1355,44 +1357,6 @@ static Error launch_bs(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t
     return Error{};
 }
 
-template <int KD, int M, int PARTS>
-static Error launch_bs6(CodeState &cs, const hipDeviceProp_t &prop, const uint8_t *const *data, uint8_t *const *par,
-                        size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
-    using Kn = bs::Bs6Kernel<KD, M, PARTS>;
-    using S = typename Kn::S;
-    const clay_code_t &c = cs.code;
-    if (int(c.k) != KD || int(c.m) != M || int(c.d) != KD + M - 1) return Error{};
-    // per-lane DMA offsets are 32-bit chunk offsets; a clamped 16-byte piece needs sc >= 64
-    if (double(S::ALPHA) * double(sc) >= 4294967296.0 || sc < 16) return Error{};
-    for (int p = 0; p < M; p++)
-        for (int i = 0; i < S::K; i++)
-            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
-                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    int dev = 0;
-    CLAY_HIP(hipGetDevice(&dev));
-    Error ae = lds_attr_once(reinterpret_cast<const void *>(&bs::k_bs6_encode<KD, M, PARTS>), Kn::LDS_BYTES, dev);
-    if (ae) return ae;
-    const int per_cu = std::max(1, int((160 * 1024) / Kn::LDS_BYTES));
-    for (size_t s = 0; s < n_stripes; s++) {
-        bs::BsArgs a{};
-        for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data[s * KD + i] : nullptr;
-        for (int x = 0; x < M; x++) a.par[x] = par[s * M + x];
-        a.sc = sc;
-        a.ntiles = uint32_t((sc + Kn::W - 1) / Kn::W);
-        a.tiles_per_xcd = (a.ntiles + 7) / 8;
-        const uint32_t max_slots = uint32_t(std::max(1, prop.multiProcessorCount / 8) * per_cu);
-        a.nslots = std::min(max_slots, a.tiles_per_xcd);
-        bs::k_bs6_encode<KD, M, PARTS><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
-        CLAY_HIP(hipGetLastError());
-        t_last_launches++;
-    }
-    char buf[64];
-    std::snprintf(buf, sizeof(buf), "bitsliced6-k%dm%d-w%d", KD, M, Kn::W);
-    t_last_path = buf;
-    *done = true;
-    return Error{};
-}
-
 // The streaming encode (stream_encode.hpp) for q = 4, t = 4 codes with k = 9 or 10.
 template <int KD, int LOADERS>
 static Error launch_stream(CodeState &cs, const DevProps &prop, const uint8_t *const *data, uint8_t *const *par,
@@ -1469,7 +1433,7 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
     const clay_code_t &c = cs.code;
     const size_t sc = chunk / c.sub_chunk_no;
     if (c.d != c.k + c.m - 1) return Error{};
-    // the LDS-DMA kernels (stream, v6) need 8-byte rows: sc % 8 == 0, 8-byte aligned chunks;
+    // the LDS-DMA kernel (stream) needs 8-byte rows: sc % 8 == 0, 8-byte aligned chunks;
     // the v1 kernel takes any sub-chunk size and alignment (byte-granular partial words)
     bool rows8 = sc % 8 == 0;
     for (size_t s = 0; s < n_stripes && rows8; s++) {
@@ -1500,15 +1464,6 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
         if (e || *done || mode == kModeStream) return e;
     }
     if (mode == kModeStream) return e;
-    // v6 (column-per-lane, 2-slot ring); tile 4 = 128-byte tiles / 5-slot ring
-    if (mode == kModeBs6) {
-        if (!rows8) return e;
-        if (key == 1004) {
-            if (tile == 4) e = launch_bs6<10, 4, 4>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
-            else e = launch_bs6<10, 4, 8>(cs, prop.raw, data, par, n_stripes, sc, stream, done);
-        }
-        return e;
-    }
     // v1 (register loads, PG x 32 positions per lane): every q = m code it is instantiated for
     switch (key) {
     case 1004:
@@ -1792,13 +1747,9 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
 // ---------------------------------------------------------------------------
 // Decode / repair on device
 // ---------------------------------------------------------------------------
-// The single-launch streaming decode (stream_decode.hpp) for q = 4, t = 4 codes with
-// k = 9 / 10: any erasure pattern of <= 4 nodes with at most one erasure per y-section (two
-// erasures in one section need a PFT pair between items of the same round: those patterns stay
-// on the plan executor).  `cin` / `cout`: internal node pointers (inputs of present nodes,
-// outputs of erased nodes, nullptr if not wanted).
-hipError_t launch_stream_decode_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
-
+// The streaming decodes (stream_decode.hpp phase A + stream_local.hpp / stream_fused2.hpp) for
+// q = 4, t = 4 codes with k = 9 / 10.  `cin` / `cout`: internal node pointers (inputs of present
+// nodes, outputs of erased nodes, nullptr if not wanted).
 // Shared by the streaming decodes: pattern checks, RS rows used, H_K^-1, the v_perm tables of
 // its rows and of A_i = H_K^-1 gamma H_i, the node loads of a tile.  *ok = false: not eligible
 // (per_sec_max: the most erasures one y-section may hold).
@@ -1885,7 +1836,7 @@ static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const 
     a.sec_off[4] = nt;
     a.nt = nt;
     if (nt == 0) return Error{};
-    // the split / local kernels stream through R - 1 buffers (the last holds tables): a step's
+    // the local kernel streams through R - 1 buffers (the last holds tables): a step's
     // loads are issued during the step before it, across tiles too (section 3 -> section 0)
     for (int y = 0; y < 4; y++)
         if (n[y] > R - 1 || n[y] + n[(y + 1) % 4] > R - 1) return Error{};
@@ -1911,87 +1862,6 @@ static Error dec_tables(CodeState &cs, const DevProps &prop, const std::vector<u
         it = cs.dtabs.emplace(key, d).first;
     }
     *out = it->second;
-    return Error{};
-}
-
-template <int KD>
-static Error launch_stream_decode(CodeState &cs, DevState &ds, const DevProps &prop, const uint8_t *const *cin,
-                                  uint8_t *const *cout, const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream,
-                                  bool split, bool *done) {
-    *done = false;
-    bs::DecArgs a;
-    std::vector<uint32_t> tabs;
-    bool ok = false;
-    // two erasures in one section need a PFT pair inside a round: not in these kernels
-    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
-    if (e || !ok) return e;
-    const uint32_t used = a.used;
-    // phase-B layer order: by iscore level (red erased sections), then by the set of red
-    // sections (uniform corrections per wave), rounds of <= 128 layers of one level
-    std::vector<std::pair<uint32_t, int>> lay;
-    for (int z = 0; z < 256; z++) {
-        uint32_t red = 0;
-        for (int y = 0; y < 4; y++)
-            if ((a.emask[y] >> ((z >> (2 * (3 - y))) & 3)) & 1u) red |= 1u << y;
-        lay.push_back({uint32_t(__builtin_popcount(red)) << 8 | red, z});
-    }
-    std::stable_sort(lay.begin(), lay.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
-    uint8_t *ord = reinterpret_cast<uint8_t *>(&tabs[bs::kDecOrder]);
-    uint32_t nr = 0;
-    for (size_t i = 0; i < lay.size(); i++) {
-        ord[i] = uint8_t(lay[i].second);
-        const bool new_level = i == 0 || (lay[i].first >> 8) != (lay[i - 1].first >> 8);
-        if (new_level || i - a.round_start[nr - 1] >= 128) {  // two layers per lane octet
-            if (nr + 1 >= sizeof(a.round_start) / sizeof(a.round_start[0])) return Error{};
-            a.round_start[nr++] = uint32_t(i);
-        }
-    }
-    a.round_start[nr] = 256;
-    a.nround = nr;
-    a.round1 = nr;
-    for (uint32_t r = 0; r < nr; r++)
-        if ((lay[a.round_start[r]].first >> 8) >= 1) {
-            a.round1 = r;
-            break;
-        }
-    // split solve: the dropped terms of every round as (layer, section Y, node X) pairs
-    {
-        uint16_t *pairs = reinterpret_cast<uint16_t *>(&tabs[bs::kDecPairs]);
-        uint32_t np = 0;
-        for (uint32_t r = 0; r < nr; r++) {
-            a.pstart[r] = np;
-            if (r < a.round1) continue;
-            for (uint32_t li = a.round_start[r]; li < a.round_start[r + 1]; li++) {
-                const uint32_t z = ord[li];
-                for (int y = 0; y < 4; y++) {
-                    const uint32_t xe = (z >> (2 * (3 - y))) & 3u;
-                    if (!((a.emask[y] >> xe) & 1u)) continue;  // section y not red in z
-                    for (uint32_t x = 0; x < 4; x++) {
-                        if (x == xe || !((used >> (4 * y + x)) & 1u)) continue;
-                        if (np >= uint32_t(bs::kDecMaxPairs)) return Error{};
-                        pairs[np++] = uint16_t(z | uint32_t(y) << 8 | x << 10);
-                    }
-                }
-            }
-        }
-        a.pstart[nr] = np;
-    }
-    const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
-    a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
-    e = dec_tables(cs, prop, tabs, stream, &a.tabs);
-    if (e) return e;
-    // split decode (k_stream_syn + k_stream_solve, S through a pooled workspace of 64 KiB per
-    // 64-byte tile) unless exec mode "stream-fused" selects the fused single-launch kernel
-    LeaseGuard ws(ds, stream);
-    if (split) {
-        Error le = lease_acquire(ds, (sc + 63) / 64 * 65536, stream, &ws.l);
-        if (le) return le;
-        a.ws = static_cast<uint8_t *>(ws.ptr());
-    }
-    CLAY_HIP(launch_stream_decode_kernel(KD, a, stream, prop.dev));
-    t_last_launches += split ? 2 : 1;
-    t_last_exec = split ? "stream-split" : "stream";
-    *done = true;
     return Error{};
 }
 
@@ -2083,8 +1953,8 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
 int launch_bs_repair_kernel(int k, int m, int y0, const bs::RepArgs &a, hipStream_t stream, int dev, int cus,
                             int stream_mode, int *launches);
 
-// One erased node with every other node present, in a q = m code (d = n - 1), exec mode
-// "codeword": when the chunks are one codeword, the erased chunk is the one a repair from all
+// One erased node with every other node present, in a q = m code (d = n - 1), through
+// clay_decode_device_codeword: when the chunks are one codeword, the erased chunk is the one a repair from all
 // n - 1 helpers rebuilds (the codeword through the k data chunks is unique: decode.rs:31-161 and
 // repair.rs:140-421 return the same bytes; on inputs that are NOT a codeword the two differ, so
 // auto keeps the decode), and the repair reads only
@@ -2121,7 +1991,7 @@ static Error decode_by_repair(const clay_code_t &c, const uint8_t *const *chunks
 }
 
 static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
-                                uint8_t *const *outs, size_t chunk, int dev, void *stream) {
+                                uint8_t *const *outs, size_t chunk, int dev, void *stream, bool codeword = false) {
     Error e = check_code(code);
     if (e) return e;
     const clay_code_t &c = *code;
@@ -2165,30 +2035,28 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         size_t in = internal_of(c, i);
         P.p[in] = chunks[i] ? const_cast<uint8_t *>(chunks[i]) : (want[in] ? outs[i] : nullptr);
     }
-    // streaming decode (q = 4, t = 4 codes, one erasure per y-section, sc % 8 == 0): exec mode
-    // "stream" always; auto from 3 erasures on, where the split kernels beat the grouped plan
-    // executor ((10,4,13) 1 GiB: 4 erasures 0.77 vs 0.92 ms, 3: 0.72 vs 0.79; 2: 0.65 vs 0.57,
-    // 1: 0.59 vs 0.42 -- profiles/r03/decode_split/)
     const int xmode = g_exec_mode.load(std::memory_order_relaxed);
     size_t n_erased = 0;
     for (size_t in = 0; in < tn; in++) n_erased += erased[in] && !(in >= c.k && in < c.k + c.nu) ? 1 : 0;
-    // exec mode "codeword" (the caller vouches that the chunks are one codeword): a single
-    // erasure is rebuilt by the repair kernel; every other decode runs as in auto
-    if (xmode == kExecCodeword && n_erased == 1 && ner == 1 && ids.size() + 1 == c.n) {
+    // clay_decode_device_codeword (the caller vouches, for this call only, that the chunks are one
+    // codeword): a single erasure is rebuilt by the repair kernel; every other decode runs as
+    // clay_decode_device does
+    if (codeword && n_erased == 1 && ner == 1 && ids.size() + 1 == c.n) {
         bool done = false;
         e = decode_by_repair(c, chunks, er[0], outs[er[0]], chunk, dev, static_cast<hipStream_t>(stream), &done);
         if (e || done) return e;
     }
-    // local decode (erasures in one section plus at most one other, stream_local.hpp): auto and
-    // exec mode "stream-local"
-    const bool autoish = xmode == kExecAuto || xmode == kExecCodeword;
-    const bool try_local = autoish || xmode == kExecStreamLocal;
-    const bool try_split = xmode == kExecStream || xmode == kExecStreamFused || (autoish && n_erased >= 3);
-    // fused decode v2 for 2-4 erasures in distinct sections: auto from 3 erasures and
-    // "stream-fused2" ((10,4,13) 1 GiB: {0,4,8,12} 0.52 ms vs 0.73 split, {0,4,8} 0.48 vs 0.62;
-    // {0,4} 0.458 vs 0.452 on the local decode; profiles/r04/fused2/)
-    const bool try_f2 = xmode == kExecStreamFused2 || (autoish && n_erased >= 3);
-    if ((try_local || try_split || try_f2) && tn == 16) {
+    // streaming decodes of q = 4, t = 4 codes (sc % 8 == 0, sc >= 512):
+    //  * the local decode (erasures in one section plus at most one other, stream_local.hpp):
+    //    auto, "stream" and "stream-local";
+    //  * the fused decode v2 (2-4 erasures in distinct sections, stream_fused2.hpp): auto from 3
+    //    erasures, "stream" and "stream-fused2" from 2 ((10,4,13) 1 GiB: {0,4,8,12} 0.52 ms vs 0.92
+    //    on the grouped executor, {0,4,8} 0.48 vs 0.79; {0,4} 0.458 vs 0.452 on the local decode;
+    //    profiles/r04/fused2/)
+    const bool stream_all = xmode == kExecStream;
+    const bool try_local = xmode == kExecAuto || stream_all || xmode == kExecStreamLocal;
+    const bool try_f2 = xmode == kExecStreamFused2 || stream_all || (xmode == kExecAuto && n_erased >= 3);
+    if ((try_local || try_f2) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};
         for (size_t i = 0; i < c.n; i++) {
@@ -2208,12 +2076,6 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         if (try_f2) {
             if (c.k == 10) e = launch_stream_fused2<10>(cs, prop, cin, cout, erased, sc, st, &done);
             else if (c.k == 9) e = launch_stream_fused2<9>(cs, prop, cin, cout, erased, sc, st, &done);
-            if (e || done) return e;
-        }
-        if (try_split) {
-            const bool split = xmode != kExecStreamFused;
-            if (c.k == 10) e = launch_stream_decode<10>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
-            else if (c.k == 9) e = launch_stream_decode<9>(cs, *ds, prop, cin, cout, erased, sc, st, split, &done);
             if (e || done) return e;
         }
     }
@@ -2245,8 +2107,8 @@ static Error repair_device_impl(const clay_code_t *code, size_t lost, const size
     // helper (no aloof nodes); auto and "stream" exec modes ((9,3,11) 256 MiB chunks: 0.345-0.357
     // vs 0.39-0.41 ms grouped on the same boxes, profiles/r03/)
     const int xm = g_exec_mode.load(std::memory_order_relaxed);
-    const bool xauto = xm == kExecAuto || xm == kExecCodeword;
-    if ((xauto || xm == kExecStream || xm == kExecStreamFused) && c.q == c.m && tn <= 16 && nh + 1 == c.n) {
+    const bool xauto = xm == kExecAuto;
+    if ((xauto || xm == kExecStream) && c.q == c.m && tn <= 16 && nh + 1 == c.n) {
         bs::RepArgs ra{};
         const size_t lost_int = internal_of(c, lost);
         bool ok = true;
@@ -2465,7 +2327,6 @@ int clay_set_encode_path(int mode) {
     switch (path) {
     case kModeAuto: case kModeStaged: case kModeFused: ok = tile == 0; break;
     case kModeBs: ok = tile == 0 || tile == 1 || tile == 4; break;     // v1 lanes of 32 B per column group
-    case kModeBs6: ok = tile == 0 || tile == 4; break;                // 256- / 128-byte tiles
     case kModeStream: ok = tile == 0 || tile == 1 || tile == 2 || tile == 4 || tile == 7; break;  // loader waves
     default: ok = false;
     }
@@ -2476,8 +2337,8 @@ int clay_set_encode_path(int mode) {
     return prev;
 }
 int clay_set_exec_mode(int mode) {
-    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream && mode != kExecStreamFused &&
-        mode != kExecStreamLocal && mode != kExecStreamFused2 && mode != kExecCodeword)
+    if (mode != kExecAuto && mode != kExecGrouped && mode != kExecTile && mode != kExecStream &&
+        mode != kExecStreamLocal && mode != kExecStreamFused2)
         return -1;
     return g_exec_mode.exchange(mode);
 }
@@ -2589,6 +2450,13 @@ int clay_decode_device(const clay_code_t *code, const uint8_t *const *chunks, co
     return e ? report(e, err) : 0;
 }
 
+int clay_decode_device_codeword(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
+                                uint8_t *const *outs, size_t chunk, int device, void *stream, clay_error_t *err) {
+    if (err) std::memset(err, 0, sizeof(*err));
+    Error e = decode_device_impl(code, chunks, er, ner, outs, chunk, device, stream, true);
+    return e ? report(e, err) : 0;
+}
+
 int clay_repair_device(const clay_code_t *code, size_t lost, const size_t *ids, const uint8_t *const *bufs, size_t nh,
                        size_t chunk, uint8_t *out, int device, void *stream, clay_error_t *err) {
     if (err) std::memset(err, 0, sizeof(*err));
@@ -2664,14 +2532,17 @@ int clay_release_captured(int device, clay_error_t *err) {
     DevState *ds;
     Error e = dev_state(device, &ds);
     if (e) return report(e, err);
-    DeviceGuard g(device);
-    // the caller has destroyed its graphs; a replay launched before may still be running
-    if (hipDeviceSynchronize() != hipSuccess)
-        return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "HIP error: device synchronize failed"), err);
+    // No device-wide synchronize here: hipDeviceSynchronize while another thread captures (global
+    // capture mode, torch.cuda.graph's default) would invalidate that capture.  The caller has
+    // waited for every replay of the graphs and destroyed them (clay.h); refuse while one of this
+    // library's calls is inside a capture right now (its table or lease is in use).
     std::lock_guard<std::mutex> lk(ds->mu);
     for (auto &t : ds->captured)
         if (t->users > 0)
             return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "a stream capture is using the pointer-table arena"), err);
+    for (auto &l : ds->pool)
+        if (l->pinned && l->busy)
+            return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "a stream capture is using a pooled workspace"), err);
     ds->captured.clear();
     ds->cap_used = 0;
     for (auto &l : ds->pool)

@@ -1,6 +1,6 @@
 // stream_encode.hpp -- the encode kernel for codes with q = 4, t = 4 (alpha = 256), e.g. the
 // BASELINE (10,4,13): loader waves stream the data through per-node LDS buffers while
-// compute waves run the bit-sliced GF(2^8) math of bitslice6.hpp.
+// compute waves run the bit-sliced GF(2^8) math of encode_math.hpp.
 //
 // Data flow per workgroup (one per CU, 160 KiB LDS):
 //  * A tile is W = 256 byte positions of every (node, layer) sub-chunk row.  It is
@@ -20,7 +20,7 @@
 //    through the choice of piece per lane (see sw() below) so the compute reads stay
 //    bank-conflict free (bench_tools/stream_probe: coalesced DMA 0.345 vs 0.375 ms
 //    memory-only for the scattered piece map of the v6 image).
-//  * Compute (8 waves, 512 lanes): lane = (column c, part).  The math is bitslice6.hpp's
+//  * Compute (8 waves, 512 lanes): lane = (column c, part).  The math is encode_math.hpp's
 //    v6 kernel: PRT in the byte domain, 8x8 bit transpose, the RS generator as
 //    compile-time XOR networks into 4 x 8 plane accumulators, PFT in registers at the end
 //    of each group, transposed back and stored.
@@ -37,7 +37,7 @@
 // so the bytes are identical to the oracle's.
 #pragma once
 
-#include "bitslice6.hpp"
+#include "encode_math.hpp"
 
 namespace clay {
 namespace bs {
@@ -103,7 +103,7 @@ struct ChipMap {
 // CSE: RS folds through compile-time common subexpressions (xor_cse.hpp)
 template <int KD, int LOADERS, int CPL = 0, int CPS = 0, bool CSE = true>
 struct StreamEnc {
-    using K6 = Bs6Kernel<KD, 4, 8>;
+    using K6 = EncMath<KD>;
     using S = typename K6::S;
     static constexpr int Q = 4, T = 4, W = 256, CWAVES = 8;
     static constexpr int BLOCK = 64 * (CWAVES + LOADERS);
@@ -338,7 +338,7 @@ struct StreamEnc {
         }
     }
     // Group G finished: red vertex C[G][z_G] = U, and the PFT pairs with groups h < G
-    // (transforms.rs:108-125) -- the v6 schedule, see Bs6Kernel::end_group.
+    // (transforms.rs:108-125) (Hold: encode_math.hpp).
     template <int G>
     __device__ static void end_group(const BsArgs &a, const uint32_t (&acc)[Q * 8], typename K6::Hold &H, int c,
                                      StreamTile t, uint32_t prel, bool ragged) {
@@ -405,9 +405,47 @@ struct StreamEnc {
 // 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1, 32 = the group whose
 // outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
 // across workgroups; only meaningful with bit 1), 2048 = chip round-robin tile map (ChipMap).
+// Segment timing of the probe instantiations (PROBE bit 4096): s_memtime cycles summed per
+// kind (compute wave: 0 barrier wait, 1 section math; loader wave: 0 vmcnt wait, 1 barrier,
+// 2 DMA issue) and per section y, plus the end-of-group work (outputs) per group g; written by
+// lane 0 of compute waves 0 and 7 and of loader wave 0 to a.par[4] (80 uint64 per workgroup:
+// records of 17 at 0, 24 and 48).
+struct TimeAcc {
+    uint64_t v[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, gend[4] = {0, 0, 0, 0};
+    uint64_t t_start = 0, t_first = 0, t_end = 0;
+    __device__ __forceinline__ void add(int kind, int y, uint64_t &t0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint64_t d = t1 - t0;
+        t0 = t1;
+        // uniform branches: the sums stay in SGPRs
+        if (y == 0) v[kind][0] += d;
+        else if (y == 1) v[kind][1] += d;
+        else v[kind][2] += d;
+    }
+    __device__ __forceinline__ void addg(int g, uint64_t &t0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint64_t d = t1 - t0;
+        t0 = t1;
+        if (g == 0) gend[0] += d;
+        else if (g == 1) gend[1] += d;
+        else if (g == 2) gend[2] += d;
+        else gend[3] += d;
+    }
+    __device__ void put(uint64_t *p, int ntile) const {
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) p[i * 3 + j] = v[i][j];
+        for (int g = 0; g < 4; g++) p[9 + g] = gend[g];
+        p[13] = t_start;
+        p[14] = t_first;
+        p[15] = t_end;
+        p[16] = uint64_t(ntile);
+    }
+};
+
 template <int KD, int LOADERS, int PROBE = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
     using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3, ((PROBE >> 10) & 1) == 0>;
+    constexpr bool TM = (PROBE & 4096) != 0;
     using K6 = typename Kn::K6;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -429,11 +467,14 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         typename Kn::Loader L;
         Kn::loader_init(L, uint32_t(a.sc), wave - Kn::CWAVES, lane);
         const uint32_t lds0 = lds_addr_of(smem);
+        TimeAcc T;
+        T.t_start = TM ? __builtin_amdgcn_s_memtime() : 0;
         if constexpr (!(PROBE & 2))
             for (int s = 0; s < 3 && s < nsteps; s++) Kn::issue_any(s % 3, a, L, lds0, tm.tile(0, slot, ns), s / 3);
         for (int s = 0; s < nsteps; s++) {
             const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
             const StreamTile t = tm.tile(k, slot, ns);
+            uint64_t t0 = TM ? __builtin_amdgcn_s_memtime() : 0;
             // step s landed: everything issued after it may stay in flight
             int after = 0;
             if (s == 0) {
@@ -449,13 +490,23 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             } else {
                 wait_vm_rt(after);
             }
+            if constexpr (TM) T.add(0, y, t0);
             lds_barrier();
+            if constexpr (TM) T.add(1, y, t0);
             // step s-1's buffers are free: refill them with step s+2
             const int s2 = s + 2;
             if (!(PROBE & 2) && s >= 1 && s2 < nsteps) {
                 const int k2 = s2 / Kn::STEPS, r2 = s2 % Kn::STEPS;
                 Kn::issue_any(r2 % 3, a, L, lds0, tm.tile(k2, slot, ns), r2 / 3);
             }
+            if constexpr (TM) {
+                T.add(2, y, t0);
+                if (s == 0) T.t_first = t0;
+            }
+        }
+        if constexpr (TM) {
+            T.t_end = __builtin_amdgcn_s_memtime();
+            if (lane == 0 && wave == Kn::CWAVES) T.put(reinterpret_cast<uint64_t *>(a.par[4]) + blockIdx.x * 80u + 48u, ntile);
         }
         return;
     }
@@ -479,8 +530,11 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             for (int s = 0; s < 3 && s < nsteps; s++) Kn::issue_any(s % 3, a, LD, lds0, tm.tile(0, slot, ns), s / 3);
     }
     int st1 = 0, st2 = 0;  // counted stores issued in steps s-1 and s-2
+    TimeAcc T;
+    T.t_start = TM ? __builtin_amdgcn_s_memtime() : 0;
     for (int s = 0; s < nsteps; s++) {
         const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
+        uint64_t t0 = TM ? __builtin_amdgcn_s_memtime() : 0;
         if constexpr (LOADERS == 0 && !(PROBE & 2)) {
             const StreamTile t = tm.tile(k, slot, ns);
             int after;
@@ -495,6 +549,10 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             }
         }
         lds_barrier();
+        if constexpr (TM) {
+            T.add(0, y, t0);
+            if (s == 0) T.t_first = t0;
+        }
         if constexpr (LOADERS == 0 && !(PROBE & 2)) {
             const int s2 = s + 2;
             if (s >= 1 && s2 < nsteps) {
@@ -518,6 +576,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             else if (y == 1) Kn::template section<1>(smem + Kn::REGION, L, acc);
             else Kn::template section<2>(smem + 2 * Kn::REGION, L, acc);
         }
+        if constexpr (TM) T.add(1, y, t0);
         if (y == 2 && !(PROBE & 4)) {
             const StreamTile t = tm.tile(k, slot, ns);
             const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
@@ -533,6 +592,12 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             st2 = st1;
             st1 = 0;
         }
+        if constexpr (TM) T.addg(g, t0);
+    }
+    if constexpr (TM) {
+        T.t_end = __builtin_amdgcn_s_memtime();
+        if (lane == 0 && (wave == 0 || wave == Kn::CWAVES - 1))
+            T.put(reinterpret_cast<uint64_t *>(a.par[4]) + blockIdx.x * 80u + (wave == 0 ? 0u : 24u), ntile);
     }
 }
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CLAY_ABI_VERSION 3
+#define CLAY_ABI_VERSION 4
 
 /* ClayCode public fields (lib.rs:59-82) + the two private RS counts (lib.rs:79-81). */
 typedef struct clay_code {
@@ -192,6 +192,21 @@ int clay_decode_device(const clay_code_t *code, const uint8_t *const *chunks,
                        const size_t *erasures, size_t n_erasures, uint8_t *const *out_chunks,
                        size_t chunk_size, int device, void *stream, clay_error_t *err);
 
+/* clay_decode_device for callers whose chunks are ONE CODEWORD (the crate's own usage: chunks
+ * that ClayCode::encode produced), chosen per call.  A decode of one erased node with every other
+ * node present, in a q = m code with a streaming repair kernel ((9,3,11), (10,4,13), (4,2,5)),
+ * rebuilds the node with the repair of repair.rs:140-421 from the whole chunks (last exec path
+ * "bs-repair-stream", when the sub-chunk gives every CU a tile): it reads only the alpha / q layers
+ * of the node's repair plane (repair.rs:61-126) instead of every layer ((10,4,13) 1 GiB {0}:
+ * 0.137 ms vs 0.386 on the local decode).  On a codeword the bytes equal decode.rs:31-161's (the
+ * codeword through the k data chunks is unique); on chunks that are NOT one codeword they differ,
+ * which is why clay_decode_device never takes this route.  Every other pattern runs exactly as
+ * clay_decode_device.  The choice is an argument of the call, not process state: concurrent
+ * clay_decode_device calls are unaffected.  No reference counterpart (decode.rs has one path). */
+int clay_decode_device_codeword(const clay_code_t *code, const uint8_t *const *chunks,
+                                const size_t *erasures, size_t n_erasures, uint8_t *const *out_chunks,
+                                size_t chunk_size, int device, void *stream, clay_error_t *err);
+
 /* Repair on device: helper buffers are device pointers (beta*sub-chunk bytes),
  * out is a device buffer of chunk_size bytes. */
 int clay_repair_device(const clay_code_t *code, size_t lost_node, const size_t *helper_ids,
@@ -214,11 +229,9 @@ int clay_repair_device_full_chunks(const clay_code_t *code, size_t lost_node, co
 
 /* Pre-allocate an idle pooled workspace for chunk_size (any stream may take it) and
  * build + upload the code's encode plan, so that a later call allocates nothing --
- * e.g. before stream capture.  The workspace is q x t x chunk_size bytes, which covers
- * every call of that chunk size: the grouped executor's U workspace (q t chunk_size)
- * and the split streaming decode's S' workspace (64 KiB per 64-byte tile of the
- * sub-chunk, i.e. 1,024 x sc bytes for sc = chunk_size / alpha: 430 MB for a 1 GiB
- * (10,4,13) stripe), each held per in-flight call.  Decode/repair plans and the
+ * e.g. before stream capture.  The workspace is q x t x chunk_size bytes, the grouped
+ * executor's U workspace for that chunk size, held per in-flight call (the streaming
+ * kernels need none).  Decode/repair plans and the
  * streaming decode's pattern tables depend on the erasure pattern: run one call per
  * pattern before capturing it (a capture that needs an unprepared one fails with
  * CLAY_ERR_DEVICE rather than allocating). */
@@ -233,9 +246,11 @@ int clay_release_workspace(int device, clay_error_t *err);
  * captured batch calls (a 4 MiB per-device arena; a captured batch of n stripes takes
  * n x 130 x 8 bytes, so about a dozen 300-stripe captures fill it, after which capturing
  * such calls fails with CLAY_ERR_DEVICE) and the pooled workspaces pinned to graphs.
- * Call it once every graph captured from this library's calls on `device` has been
- * destroyed; it synchronises the device first (a replay may still run).  Fails while a
- * capture that uses the arena is in progress.  No reference counterpart. */
+ * Call it once every replay of the graphs captured from this library's calls on `device` has
+ * completed (synchronise the replay streams) and the graphs are destroyed.  It does not
+ * synchronise the device itself, so it is safe while other threads capture unrelated work;
+ * it fails (nothing released) while one of this library's calls is inside a capture at that
+ * moment.  No reference counterpart. */
 int clay_release_captured(int device, clay_error_t *err);
 
 /* Bytes of device memory held by the device's buffer pool (tests / monitoring). */
@@ -248,68 +263,56 @@ size_t clay_workspace_bytes(int device);
  *                  compiled instantiation; else the byte-sliced fused kernel when the
  *                  parity is one y-section; else the staged plan executor.  Batches of
  *                  >= 4 stripes of <= 4 MiB of data run as one staged launch per level.
- *                  The LDS-DMA kernels (stream, bitsliced6) need sub-chunks that are
+ *                  The LDS-DMA kernel (stream) needs sub-chunks that are
  *                  multiples of 8 bytes and 8-byte aligned chunk pointers (else auto
  *                  falls through); the v1 kernel takes any sub-chunk size and alignment.
  *   1 staged    -- the plan executor (k_gexec), any code
  *   2 fused     -- byte-sliced fused kernel (q == m <= 4)
  *   3 bitsliced -- bit-sliced v1 (register loads); variant = lanes per column group
  *                  for (10,4,13): 0 (2), 1, 4
- *   4 bitsliced6-- v6 (column-per-lane, 2-slot LDS ring), (10,4,13); variant 0 = 256-B
- *                  tiles, 4 = 128-B tiles
  *   5 stream    -- the streaming kernel (stream_encode.hpp); variant = loader waves
  *                  for (10,4,13): 0 (= 4, the default), 1, 2, 4; (9,4,12) always runs
  *                  4 loader waves (its variant is accepted and ignored); (9,3,11): 7 loader
  *                  waves for variant 7, else 2 (stream_encode3.hpp)
- * Bits 8..15 = variant.  Every accepted (path, variant) produces the reference's
+ * (4, the v6 kernel of round 1, is retired.)  Bits 8..15 = variant.  Every accepted (path, variant) produces the reference's
  * parity bytes; any other value returns -1 and leaves the setting unchanged.
  * Returns the previous setting (path | variant << 8). */
 int clay_set_encode_path(int mode);
 
 /* Plan executor for decode, repair and the staged encode (process-wide tuning knob; no
- * reference counterpart -- the crate has one CPU path):
+ * reference counterpart -- the crate has one CPU path).  A mode only chooses kernels: every
+ * mode returns the reference's bytes on any input.
  *   0 auto    -- the tile-fused executor (one launch, U workspace in LDS) for small plans
  *                (<= 32 op groups) whose U slots fit the LDS budget, else the grouped
- *                per-level executor; decodes of >= 3 erasures of q = 4, t = 4 codes
- *                ((10,4,13), (9,4,12)) in distinct y-sections with sc % 8 == 0, sc >= 512 run
- *                the split streaming decode (k_stream_syn + k_stream_solve, last path
- *                "stream-split") -- when the ring fits (every 3- and 4-erasure pattern of
- *                (10,4,13), the BASELINE {0,4,8,12} included) the fused decode v2 instead
- *                (k_stream_fused2, "stream-fused2");
- *                decodes of those codes whose erasures lie in one y-section
- *                plus at most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4},
- *                {0,1,2,3}, ...) run the single-launch local decode (k_stream_local,
- *                "stream-local")
+ *                per-level executor; for q = 4, t = 4 codes ((10,4,13), (9,4,12)) with
+ *                sc % 8 == 0, sc >= 512: decodes whose erasures lie in one y-section plus at
+ *                most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4}, {0,1,2,3},
+ *                ...) run the single-launch local decode (k_stream_local, last path
+ *                "stream-local"); 3 or 4 erasures in distinct y-sections (the BASELINE
+ *                {0,4,8,12} included) the fused decode v2 (k_stream_fused2, "stream-fused2")
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
  *   (auto and stream: repair of (9,3,11), (10,4,13), (4,2,5) from all n - 1 other nodes runs
  *    the bit-sliced repair kernels: k_bs_repair_stream (LDS-DMA streaming, one workgroup per
  *    CU; auto when the sub-chunk gives every CU a tile, stream for any sub-chunk >= 16 bytes
  *    of (9,3,11) / (10,4,13); last path "bs-repair-stream"), else k_bs_repair ("bs-repair"))
- *   3 stream  -- every eligible decode of q = 4, t = 4 codes (any erasure count) on the split
- *                streaming decode ("stream-split"); everything else as auto
- *   4 stream-fused -- as stream, but on the fused single-launch k_stream_decode ("stream")
+ *   3 stream  -- every decode a streaming kernel takes on it: the local decode where it takes
+ *                the pattern, else the fused decode v2 (2-4 erasures in distinct sections);
+ *                everything else as auto
  *   5 stream-local -- every decode the local kernel takes on it ("stream-local"); else as auto
  *   6 stream-fused2 -- decodes of 2-4 erasures in distinct y-sections on the fused decode v2
  *                (k_stream_fused2, "stream-fused2"; ring of 10 - e node buffers: any two
  *                neighbouring sections hold <= 10 - e surviving real nodes); else as auto
- *   7 codeword -- as auto, for callers whose chunks are one codeword (the crate's usage: chunks
- *                it encoded): a decode of ONE erased node with every other node present, in a
- *                q = m code ((9,3,11), (10,4,13)), is rebuilt by k_bs_repair_stream from the whole
- *                chunks ("bs-repair-stream"; when the sub-chunk gives every CU a tile), reading the
- *                alpha / q layers of the node's repair plane of each chunk instead of every layer
- *                ((10,4,13) 1 GiB {0}: 0.16 ms vs 0.39 on the local decode).  On a codeword the
- *                bytes equal decode.rs's (the codeword through k chunks is unique); on inputs that
- *                are not a codeword they differ, which is why auto keeps the decode.
+ * (4 and 7 are retired: the single-launch decode of round 3 and the process-wide "codeword"
+ * mode, now the per-call clay_decode_device_codeword.)
  * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
  * (planner and executor tuning) are read once when the library is loaded.
- * Every mode but codeword produces the reference's bytes on any input; codeword does on
- * codewords.  Returns the previous mode, or -1 for an unknown mode (setting unchanged). */
+ * Returns the previous mode, or -1 for an unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
- * "tile" (k_texec), "grouped" (k_gexec), "stream-split" (k_stream_syn + k_stream_solve),
- * "stream" (k_stream_decode), "stream-local" (k_stream_local), "stream-fused2" (k_stream_fused2), "bs-repair-stream" (k_bs_repair_stream), "bs-repair"
- * (k_bs_repair) or "none". */
+ * "tile" (k_texec), "grouped" (k_gexec), "stream-local" (k_stream_local), "stream-fused2"
+ * (k_stream_fused2), "bs-repair-stream" (k_bs_repair_stream), "bs-repair" (k_bs_repair) or
+ * "none". */
 const char *clay_last_exec_path(void);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */

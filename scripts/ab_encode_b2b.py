@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import clay_amd  # noqa: E402
 from clay_amd import ClayCode  # noqa: E402
 
-variants = [(v.split(":")[0], int(v.split(":")[1]) if ":" in v else 0) for v in sys.argv[1:]] or [("bitsliced6", 0)]
+variants = [(v.split(":")[0], int(v.split(":")[1]) if ":" in v else 0) for v in sys.argv[1:]] or [("stream", 0)]
 code = ClayCode(10, 4, 13)
 chunk = code.encoded_chunk_size(1 << 30)
 data = torch.randint(0, 256, (10, chunk), dtype=torch.uint8, device="cuda")

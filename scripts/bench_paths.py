@@ -17,7 +17,7 @@ import clay_amd  # noqa: E402
 from clay_amd import ClayCode  # noqa: E402
 
 RUNS = int(os.environ.get("RUNS", "10"))
-EXEC = os.environ.get("CLAY_EXEC", "auto")  # plan executor: auto | grouped | tile
+EXEC = os.environ.get("CLAY_EXEC", "auto")  # exec mode: auto | grouped | tile | stream | stream-local | stream-fused2
 clay_amd.set_exec_mode(EXEC)
 stream = torch.cuda.current_stream()
 
@@ -80,26 +80,34 @@ def encode_batch_cfg(k, m, d, stripe, n):
            {"input_GiBps": round(n * k * chunk / (ms * 1e-3) / 2**30, 1)})
 
 
-def decode_cfg(k, m, d, stripe, er, mode=None):
+def decode_cfg(k, m, d, stripe, er, mode=None, codeword=False):
     prev = clay_amd.set_exec_mode(mode) if mode else None
     try:
-        _decode_cfg(k, m, d, stripe, er)
+        _decode_cfg(k, m, d, stripe, er, codeword)
     finally:
         if prev:
             clay_amd.set_exec_mode(prev)
 
 
-def _decode_cfg(k, m, d, stripe, er):
+def _decode_cfg(k, m, d, stripe, er, codeword=False):
     c = ClayCode(k, m, d)
     chunk = c.encoded_chunk_size(stripe)
     full = rnd(c.n, chunk, 2)
     outs = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
     ins = [None if i in er else full[i] for i in range(c.n)]
     ous = [outs[i] if i in er else None for i in range(c.n)]
-    ms, mn = timed(lambda: c.decode_device(ins, er, ous, chunk, 0, stream.cuda_stream))
+    ms, mn = timed(lambda: c.decode_device(ins, er, ous, chunk, 0, stream.cuda_stream, codeword=codeword))
     ndata = sum(1 for e in er if e < k)
-    report(f"decode ({k},{m},{d}) {stripe >> 20} MiB erasures {er}", ms, mn,
-           (c.n - len(er)) * chunk + ndata * chunk, {"writes_counted": "erased data nodes only"})
+    name = f"decode ({k},{m},{d}) {stripe >> 20} MiB erasures {er}"
+    if codeword and clay_amd.last_exec_path() == "bs-repair-stream":
+        # the repair route reads the beta = alpha / q layers of every other chunk and writes the
+        # erased chunk: charged the bytes it moves (a decode's full-read bytes would put frac > 1)
+        beta_bytes = chunk // c.q
+        report(name + " codeword", ms, mn, (c.n - 1) * beta_bytes + chunk,
+               {"bytes_counted": "repair route: (n-1) x chunk/q read + the erased chunk written"})
+    else:
+        report(name + (" codeword" if codeword else ""), ms, mn, (c.n - len(er)) * chunk + ndata * chunk,
+               {"writes_counted": "erased data nodes only"})
 
 
 def repair_cfg(k, m, d, chunk, lost):
@@ -144,8 +152,7 @@ if __name__ == "__main__":
             ("batch", lambda: encode_batch_cfg(4, 2, 5, 1 << 20, 256)),
             ("decode", lambda: decode_cfg(4, 2, 5, 64 << 20, [0])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
-            ("split", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "stream")),
-            ("split", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "stream-fused2")),
+            ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "grouped")),
             # the fused decode v2 for 3 and 2 erasures in distinct sections (auto: split / local)
             ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8], "stream-fused2")),
             ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),
@@ -161,12 +168,12 @@ if __name__ == "__main__":
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4])),
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 2, 3])),
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [12])),
-            # exec mode "codeword": one erasure rebuilt by the repair kernel from whole chunks
-            # (algorithmic bytes still counted as a decode's: every survivor + the output)
-            ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [0], "codeword")),
-            ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [12], "codeword")),
+            # clay_decode_device_codeword: one erasure rebuilt by the repair kernel from whole
+            # chunks (charged the repair route's bytes)
+            ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [0], codeword=True)),
+            ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [12], codeword=True)),
             ("codeword", lambda: decode_cfg(9, 3, 11, 9 * (256 << 20), [0])),
-            ("codeword", lambda: decode_cfg(9, 3, 11, 9 * (256 << 20), [0], "codeword")),
+            ("codeword", lambda: decode_cfg(9, 3, 11, 9 * (256 << 20), [0], codeword=True)),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 0)),
             ("repair", lambda: repair_cfg(9, 3, 11, 268_435_458, 11)),
             ("repair", lambda: repair_cfg(10, 4, 13, 107_374_592, 0)),

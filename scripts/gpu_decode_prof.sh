@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel trace of the (10,4,13) 1 GiB 4-erasure decode {0,4,8,12} (scripts/prof_decode.py) under
-# the executor CLAY_EXEC (default stream = split streaming decode).
+# the executor CLAY_EXEC (default stream: the local decode or the fused decode v2).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=${1:-dprof}

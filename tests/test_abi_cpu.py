@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared_functions())
 
 
-SHIPPING_KERNELS = {"k_stream_encode", "k_stream_decode", "k_stream_syn", "k_stream_solve", "k_stream_local", "k_stream_fused2", "k_stream_encode3", "k_bs_repair", "k_bs_repair_stream", "k_bs_encode", "k_bs6_encode", "k_fused_encode", "k_gexec", "k_texec", "k_ygroup"}
+SHIPPING_KERNELS = {"k_stream_encode", "k_stream_local", "k_stream_fused2", "k_stream_encode3", "k_bs_repair",
+                    "k_bs_repair_stream", "k_bs_encode", "k_fused_encode", "k_gexec", "k_texec", "k_ygroup"}
 
 
 def kernel_names(blob: bytes):
@@ -51,7 +52,7 @@ def test_library_is_gfx950_hip_binary():
     path = _lib.LIB_PATH
     blob = open(path, "rb").read()
     assert b"gfx950" in blob, "no gfx950 code object in libclay_amd.so"
-    assert _lib.lib().clay_abi_version() == 3
+    assert _lib.lib().clay_abi_version() == 4
 
 
 def test_library_ships_only_parity_producing_kernels():
@@ -78,3 +79,20 @@ def test_no_cpu_fallback_without_gpu():
         c.encode(b"needs a GPU")
     with pytest.raises(DeviceError):
         c.encode_device([1] * 4, [2] * 2, 16)
+
+
+def test_exec_modes_only_choose_kernels():
+    """Retired modes are rejected: 4 (the round-3 single-launch decode) and 7 (the process-wide
+    "codeword" mode, which changed the bytes concurrent decodes returned; now the per-call
+    clay_decode_device_codeword).  No GPU needed: the setter is host state."""
+    import clay_amd
+    L = _lib.lib()
+    assert L.clay_set_exec_mode(4) == -1 and L.clay_set_exec_mode(7) == -1
+    for name in ("codeword", "stream-fused"):
+        with pytest.raises(ValueError):
+            clay_amd.set_exec_mode(name)
+    prev = clay_amd.set_exec_mode("stream")
+    assert clay_amd.set_exec_mode(prev) == "stream"
+    assert L.clay_set_encode_path(4) == -1  # the retired v6 encode
+    with pytest.raises(ValueError):
+        clay_amd.set_encode_path("bitsliced6")

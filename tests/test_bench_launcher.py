@@ -88,8 +88,10 @@ def test_bench_launcher_builds_stale_oracle_once(oracle_mod, tmp_path):
     rank starts -- instead of N ranks running make on, and loading, the same file at once."""
     src = os.path.join(ROOT, "oracle", "clay_oracle.c")
     so = os.path.join(ROOT, "oracle", "liboracle.so")
-    st = os.stat(so)
-    os.utime(src, (st.st_atime, st.st_mtime + 5))  # the source is now newer than the library
+    src_st = os.stat(src)
+    # make the library stale by moving it into the past (never the source into the future: a
+    # future source mtime would keep every later build in other processes rebuilding)
+    os.utime(so, (src_st.st_atime - 10, src_st.st_mtime - 10))
     log = tmp_path / "make.log"
     wrapper = tmp_path / "make"
     wrapper.write_text(f"#!/bin/sh\necho \"$@\" >> {log}\nexec /usr/bin/make \"$@\"\n")
@@ -99,9 +101,12 @@ def test_bench_launcher_builds_stale_oracle_once(oracle_mod, tmp_path):
     env["OMP_NUM_THREADS"] = "1"
     env["PATH"] = f"{tmp_path}:{env.get('PATH', '')}"
     stripe = 10 * 256 * 2 * 64
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-dry",
-                        "--stripe-bytes", str(stripe), "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"],
-                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-dry",
+                            "--stripe-bytes", str(stripe), "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"],
+                           capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    finally:
+        os.utime(src, (src_st.st_atime, src_st.st_mtime))  # the source's times are untouched
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert all(d["per_rank"]["verified"])

@@ -1,9 +1,12 @@
-"""GPU tests of exec mode "codeword": a decode of one erased node with every other chunk present,
-in a q = m code, is rebuilt by the streaming repair kernel (k_bs_repair_stream) from the whole
-chunks.  The reference's decode (decode.rs:31-161) and repair (repair.rs:140-421) return the same
-bytes whenever the chunks are one codeword, so the inputs here are codewords encoded by the oracle
-and every rebuilt chunk (data or parity) must equal the encoded one bit for bit.  Other patterns
-and sizes run as in auto."""
+"""GPU tests of clay_decode_device_codeword (ClayCode.decode_device(..., codeword=True)): a decode of
+one erased node with every other chunk present, in a q = m code, is rebuilt by the streaming repair
+kernel (k_bs_repair_stream) from the whole chunks.  The reference's decode (decode.rs:31-161) and
+repair (repair.rs:140-421) return the same bytes whenever the chunks are one codeword, so the inputs
+here are codewords encoded by the oracle and every rebuilt chunk (data or parity) must equal the
+encoded one bit for bit.  Other patterns and sizes run as clay_decode_device.  The choice is per
+call: a concurrent clay_decode_device of arbitrary chunks keeps the reference decode's bytes."""
+import threading
+
 import numpy as np
 import pytest
 
@@ -13,18 +16,15 @@ from clay_amd import ClayCode
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def codeword_mode():
-    prev = clay_amd.set_exec_mode("codeword")
-    yield
-    clay_amd.set_exec_mode(prev)
-
-
-def _decode_dev(torch, c, full, er, chunk):
+def _decode_dev(torch, c, full, er, chunk, codeword=True, stream=None):
     outs = torch.full((c.n, chunk), 0xA5, dtype=torch.uint8, device="cuda")
+    sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
     c.decode_device([None if i in er else full[i] for i in range(c.n)], er,
-                    [outs[i] if i in er else None for i in range(c.n)], chunk)
-    torch.cuda.synchronize()
+                    [outs[i] if i in er else None for i in range(c.n)], chunk, 0, sh, codeword=codeword)
+    if stream is not None:
+        stream.synchronize()
+    else:
+        torch.cuda.synchronize()
     return outs
 
 
@@ -32,7 +32,7 @@ def _decode_dev(torch, c, full, er, chunk):
 # kernel (256 B for (10,4,13), 512 B for (9,3,11)), ragged ends included (sc = 2 mod 8 for (9,3,11))
 @pytest.mark.parametrize("cfg,sc,lost", [((10, 4, 13), 65536 + 40, [0, 5, 9, 10, 13]),
                                          ((9, 3, 11), 131072 + 2, [0, 4, 8, 11])])
-def test_codeword_single_erasure_runs_repair(oracle_mod, torch_cuda, codeword_mode, cfg, sc, lost):
+def test_codeword_single_erasure_runs_repair(oracle_mod, torch_cuda, cfg, sc, lost):
     torch = torch_cuda
     c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
     chunk = c.sub_chunk_no * sc
@@ -46,7 +46,7 @@ def test_codeword_single_erasure_runs_repair(oracle_mod, torch_cuda, codeword_mo
         assert int((outs[(e + 1) % c.n] != 0xA5).sum().item()) == 0
 
 
-def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda, codeword_mode):
+def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda):
     """Two erasures, and one erasure at a sub-chunk too small for every CU to get a tile: the
     paths auto takes (local decode), bit-exact."""
     torch = torch_cuda
@@ -61,20 +61,59 @@ def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda, codeword_mode):
             assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (sc, er, e)
 
 
-def test_auto_keeps_decode_semantics_on_non_codewords(oracle_mod, torch_cuda):
-    """auto never takes the repair route: on random (non-codeword) chunks a single-erasure decode
-    at the same size still returns the reference decode's bytes."""
+def test_plain_decode_keeps_decode_semantics_on_non_codewords(oracle_mod, torch_cuda):
+    """clay_decode_device never takes the repair route: on random (non-codeword) chunks a
+    single-erasure decode at the same size still returns the reference decode's bytes."""
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     sc = 65536 + 40
     chunk = c.sub_chunk_no * sc
     chunks = np.random.default_rng(3).integers(0, 256, (c.n, chunk), dtype=np.uint8)
-    prev = clay_amd.set_exec_mode("auto")
-    try:
-        outs = _decode_dev(torch, c, torch.from_numpy(chunks).cuda(), [2], chunk)
-        assert clay_amd.last_exec_path() == "stream-local"
-    finally:
-        clay_amd.set_exec_mode(prev)
+    outs = _decode_dev(torch, c, torch.from_numpy(chunks).cuda(), [2], chunk, codeword=False)
+    assert clay_amd.last_exec_path() == "stream-local"
     av = {i: chunks[i] for i in range(c.n) if i != 2}
     ref = np.frombuffer(o.decode(av, [2]), dtype=np.uint8).reshape(c.k, -1)
     assert np.array_equal(outs[2].cpu().numpy(), ref[2])
+
+
+def test_codeword_call_does_not_change_concurrent_decodes(oracle_mod, torch_cuda):
+    """Thread A decodes a codeword through the codeword entry point while thread B decodes random
+    (non-codeword) chunks through clay_decode_device, interleaved, each on its own stream: B's
+    bytes are the reference decode's every time (with a process-wide mode they were not)."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    sc = 65536 + 40
+    chunk = c.sub_chunk_no * sc
+    ref = o.encode_array(np.random.default_rng(11).integers(0, 256, c.k * chunk, dtype=np.uint8))
+    cw = torch.from_numpy(ref).cuda()
+    rnd = np.random.default_rng(12).integers(0, 256, (c.n, chunk), dtype=np.uint8)
+    rd = torch.from_numpy(rnd).cuda()
+    want_b = np.frombuffer(o.decode({i: rnd[i] for i in range(c.n) if i != 2}, [2]), dtype=np.uint8).reshape(c.k, -1)[2]
+    errors, paths = [], {"a": set(), "b": set()}
+    start = threading.Barrier(2)
+
+    def thread_a():
+        s = torch.cuda.Stream()
+        start.wait()
+        for _ in range(12):
+            out = _decode_dev(torch, c, cw, [2], chunk, codeword=True, stream=s)
+            paths["a"].add(clay_amd.last_exec_path())
+            if not np.array_equal(out[2].cpu().numpy(), ref[2]):
+                errors.append("codeword decode")
+
+    def thread_b():
+        s = torch.cuda.Stream()
+        start.wait()
+        for _ in range(12):
+            out = _decode_dev(torch, c, rd, [2], chunk, codeword=False, stream=s)
+            paths["b"].add(clay_amd.last_exec_path())
+            if not np.array_equal(out[2].cpu().numpy(), want_b):
+                errors.append("plain decode of random chunks changed")
+
+    ts = [threading.Thread(target=thread_a), threading.Thread(target=thread_b)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    assert paths == {"a": {"bs-repair-stream"}, "b": {"stream-local"}}, paths

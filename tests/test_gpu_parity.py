@@ -100,6 +100,32 @@ def test_stream3_encode_matches_oracle(oracle_mod, loaders, sc):
     assert np.array_equal(got, ref), (sc, loaders)
 
 
+@pytest.mark.parametrize("loaders", [2, 7])
+@pytest.mark.parametrize("sc", [17, 511, 513, 512 * 256 + 37])
+def test_stream3_encode_odd_subchunk(oracle_mod, torch_cuda, loaders, sc):
+    """Odd sub-chunks, which only the device API reaches (ClayCode::encode pads to an even sc,
+    encode.rs:33-39), on the (9,3,11) streaming kernel.  Every byte offset of the sub-chunks is an
+    independent codeword, so the reference parity of the odd layout is the oracle's parity of the
+    even layout sc + 1 restricted to positions [0, sc) of every sub-chunk (encode.rs:57-68)."""
+    torch = torch_cuda
+    c, o = ClayCode(9, 3, 11), oracle_mod.OracleClay(9, 3, 11)
+    alpha = c.sub_chunk_no
+    wide = o.encode_array(rand_bytes(sc + 5 * loaders, 9 * alpha * (sc + 1)))
+    assert wide.shape[1] == alpha * (sc + 1)
+    narrow = np.ascontiguousarray(wide.reshape(c.n, alpha, sc + 1)[:, :, :sc].reshape(c.n, alpha * sc))
+    chunk = alpha * sc
+    dev = torch.from_numpy(narrow[:9].copy()).cuda()
+    par = torch.full((3, chunk), 0xA5, dtype=torch.uint8, device="cuda")
+    set_encode_path("stream", loaders)
+    try:
+        c.encode_device([dev[i] for i in range(9)], [par[i] for i in range(3)], chunk)
+        torch.cuda.synchronize()
+        assert last_encode_path().startswith("stream3"), last_encode_path()
+    finally:
+        set_encode_path("auto", 0)
+    assert np.array_equal(par.cpu().numpy(), narrow[9:]), (sc, loaders)
+
+
 STREAM_SC = [16, 24, 64, 72, 104, 128, 256, 1064, 6440, 8 * 256 * 32, 8 * 256 * 32 + 8, 64 * 300 + 40,
              64 * 2000 + 8, 8 * 256 * 32 * 3 + 4096 + 24]
 
@@ -125,24 +151,10 @@ def test_stream_encode_matches_oracle(oracle_mod, cfg, loaders, sc):
     assert np.array_equal(got, ref), (cfg, sc, loaders)
 
 
-@pytest.mark.parametrize("tile", [0, 4])
-@pytest.mark.parametrize("sc", [64, 72, 1064, 64 * 300 + 40, 64 * 2000 + 8])
-def test_bitsliced6_encode_matches_oracle(oracle_mod, sc, tile):
-    """v6 (10,4,13): ragged last tile, sc % 16 == 8, more tiles than workgroups."""
-    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
-    n = 10 * c.sub_chunk_no * sc - 7
-    data = rand_bytes(sc, n)
-    ref = o.encode_array(data)
-    set_encode_path("bitsliced6", tile)
-    got = c.encode_array(data)
-    assert last_encode_path().startswith("bitsliced6"), last_encode_path()
-    assert np.array_equal(got, ref), sc
-
-
 def test_encode_path_rejects_unknown_variants():
     """Only paths that produce the reference's parity are selectable."""
     with pytest.raises(ValueError):
-        set_encode_path("bitsliced6", 40)
+        set_encode_path("bitsliced", 40)
     with pytest.raises(ValueError):
         set_encode_path("stream", 3)
     with pytest.raises(ValueError):
@@ -407,8 +419,8 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
     # every encode kernel at the BASELINE size (sc = 419,432: ragged last tile, 8-byte
     # aligned sub-chunks), auto first
     for path, tile, prefix in [("auto", 0, "stream-k10m4-w256-l4"), ("stream", 1, "stream-k10m4-w256-l1"),
-                               ("stream", 2, "stream-k10m4-w256-l2"), ("bitsliced6", 0, "bitsliced6-k10m4-w256"),
-                               ("bitsliced", 0, "bitsliced-k10m4"), ("fused", 0, "fused")]:
+                               ("stream", 2, "stream-k10m4-w256-l2"), ("bitsliced", 0, "bitsliced-k10m4"),
+                               ("fused", 0, "fused")]:
         par = torch.zeros((4, chunk), dtype=torch.uint8, device="cuda")
         set_encode_path(path, tile)
         c.encode_device([dev[i] for i in range(10)], [par[i] for i in range(4)], chunk)
@@ -418,10 +430,10 @@ def test_cfg4_10_4_13_1GiB_encode_device(oracle_mod, torch_cuda):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("mode,path", [("auto", "stream-fused2"), ("stream", "stream-split"), ("grouped", "grouped")])
+@pytest.mark.parametrize("mode,path", [("auto", "stream-fused2"), ("grouped", "grouped")])
 def test_cfg5_10_4_13_1GiB_decode_4_erasures(oracle_mod, torch_cuda, mode, path):
-    """BASELINE config 5 on random (non-codeword) chunks under the auto executor (the split
-    streaming decode) and the grouped plan executor."""
+    """BASELINE config 5 on random (non-codeword) chunks under the auto executor (the fused
+    decode v2) and the grouped plan executor."""
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     rng = np.random.default_rng(5)

@@ -97,9 +97,9 @@ def test_host_api_concurrent_threads(oracle_mod, torch_cuda):
     assert not errors, errors
 
 
-@pytest.mark.parametrize("er,path", [([1, 2, 5, 6], "grouped"), ([0, 4, 8, 12], "stream-split")])
+@pytest.mark.parametrize("er,path", [([1, 2, 5, 6], "grouped"), ([0, 4, 8, 12], "stream-fused2")])
 def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path):
-    prev = clay_amd.set_exec_mode("stream" if path == "stream-split" else "auto")
+    prev = clay_amd.set_exec_mode("auto")
     try:
         _workspace_pool_reuse(oracle_mod, torch_cuda, er, path)
     finally:
@@ -108,7 +108,7 @@ def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path):
 
 def _workspace_pool_reuse(oracle_mod, torch_cuda, er, path):
     """Decodes on 8 distinct, short-lived streams one after another reuse the pooled
-    workspace (the grouped executor's U workspace, the split decode's S workspace): the pool
+    workspace (the grouped executor's U workspace; the fused decode v2 needs none): the pool
     does not grow per stream (it grew by one workspace per stream handle before the pool
     existed)."""
     torch = torch_cuda
@@ -130,8 +130,8 @@ def _workspace_pool_reuse(oracle_mod, torch_cuda, er, path):
             assert np.array_equal(outs[e].cpu().numpy(), ref[e])
         sizes.append(clay_amd.workspace_bytes(0))
         del st
-    # one U workspace (q t = 16 nodes), or one S workspace (64 KiB per 64-byte tile)
-    assert sizes[0] >= (16 * chunk if path == "grouped" else (sc + 63) // 64 * 65536)
+    # one U workspace (q t = 16 nodes); the fused decode v2 takes none
+    assert sizes[0] >= 16 * chunk if path == "grouped" else sizes[0] == 0
     assert sizes[-1] == sizes[0], sizes
     clay_amd.release_workspace(0)
     assert clay_amd.workspace_bytes(0) == 0
@@ -437,9 +437,9 @@ def test_capture_arena_reclaimed(oracle_mod, torch_cuda):
         clay_amd.release_captured(0)
 
 
-@pytest.mark.parametrize("mode,path", [("stream", "stream-split"), ("auto", "stream-fused2")])
+@pytest.mark.parametrize("mode,path", [("grouped", "grouped"), ("auto", "stream-fused2")])
 def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda, mode, path):
-    """A 4-erasure (10,4,13) decode inside a stream capture, on the split streaming decode (its S'
+    """A 4-erasure (10,4,13) decode inside a stream capture, on the grouped executor (its U
     workspace lease covered by the reserved workspace) and on the fused decode v2 (no workspace):
     one eager call of the pattern prepared its tables, so the capture allocates nothing (the pool
     does not grow) and replays bit-exact on new data.  A pattern never run before fails inside the
@@ -462,7 +462,7 @@ def _decode_graph_capture(oracle_mod, torch_cuda, path):
     clay_amd.release_workspace(0)
     c.reserve_workspace(chunk)
     reserved = clay_amd.workspace_bytes(0)
-    assert reserved >= (sc + 63) // 64 * 65536
+    assert reserved >= c.q * c.t * chunk
     full = torch.from_numpy(_stripe(o, 10, chunk, 77)).cuda()
     outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
     args = ([None if j in er else full[j] for j in range(14)], er, [outs[j] if j in er else None for j in range(14)])

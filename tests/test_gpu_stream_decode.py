@@ -1,8 +1,9 @@
-"""GPU parity of the single-launch streaming decode (stream_decode.hpp) against the oracle.
+"""GPU parity of the streaming decodes (stream_decode.hpp phase A + the local decode,
+stream_local.hpp, and the fused decode v2, stream_fused2.hpp) against the oracle.
 
-The kernel serves q = 4, t = 4 codes ((10,4,13) and (9,4,12)) for every erasure pattern with
-at most one erasure per y-section (decode.rs:167-257 with the reference's iscore order), in
-the "stream" executor mode.  Inputs are random, i.e. NOT codewords: only the reference's exact RS row
+The kernels serve q = 4, t = 4 codes ((10,4,13) and (9,4,12)) in the "stream" executor mode: the
+local decode for erasures in one y-section plus at most one other, the fused decode v2 for 2-4
+erasures in distinct y-sections (decode.rs:167-257 with the reference's iscore order).  Inputs are random, i.e. NOT codewords: only the reference's exact RS row
 choice (reconstruct from the first k+nu present shards, decode.rs:374) reproduces those bytes,
 so these tests pin the syndrome formulation's "used" / "ignored" shard handling as well."""
 import itertools
@@ -37,12 +38,28 @@ def _patterns(c, seed, n3, n4):
     return pats
 
 
-@pytest.fixture(params=["split", "fused"])
-def auto_exec(request):
-    """exec mode "stream": the split decode (k_stream_syn + k_stream_solve), or "stream-fused":
-    the fused single-launch kernel; yields the path name last_exec_path() reports."""
-    prev = clay_amd.set_exec_mode("stream" if request.param == "split" else "stream-fused")
-    yield "stream-split" if request.param == "split" else "stream"
+def local_eligible(c, er):
+    """k_stream_local: erasures in one y-section plus at most one erasure in one other section."""
+    per = [0] * c.t
+    for e in er:
+        per[_internal(c, e) // c.q] += 1
+    busy = [n for n in per if n]
+    return len(busy) == 1 or (len(busy) == 2 and min(busy) == 1)
+
+
+def stream_path(c, er):
+    """The kernel exec mode "stream" runs a pattern on (None: the plan executor)."""
+    if local_eligible(c, er):
+        return "stream-local"
+    if fused2_eligible(c, er):
+        return "stream-fused2"
+    return None
+
+
+@pytest.fixture
+def stream_mode():
+    prev = clay_amd.set_exec_mode("stream")
+    yield
     clay_amd.set_exec_mode(prev)
 
 
@@ -66,9 +83,9 @@ def _oracle_erased(o, c, chunks, er):
 
 @pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
 @pytest.mark.parametrize("sc", [512, 520, 64 * 37 + 40])
-def test_stream_decode_patterns_random_inputs(oracle_mod, torch_cuda, auto_exec, cfg, sc):
+def test_stream_decode_patterns_random_inputs(oracle_mod, torch_cuda, stream_mode, cfg, sc):
     """Every 1- and 2-erasure pattern and a sample of 3- and 4-erasure patterns on random
-    (non-codeword) chunks: the erased data chunks match the oracle bit for bit; the stream
+    (non-codeword) chunks: the erased data chunks match the oracle bit for bit; a streaming
     kernel ran for every eligible pattern (the rest fall back to the plan executor)."""
     torch = torch_cuda
     c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
@@ -79,8 +96,8 @@ def test_stream_decode_patterns_random_inputs(oracle_mod, torch_cuda, auto_exec,
         chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
         got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
         path = clay_amd.last_exec_path()
-        if stream_eligible(c, er):
-            assert path == auto_exec, (er, path)
+        if stream_path(c, er):
+            assert path == stream_path(c, er), (er, path)
             n_stream += 1
         ref = _oracle_erased(o, c, chunks, er)
         for e in er:
@@ -93,7 +110,7 @@ def test_stream_decode_patterns_random_inputs(oracle_mod, torch_cuda, auto_exec,
 
 @pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
 @pytest.mark.parametrize("sc", [520, 64 * 8 * 33 + 24])
-def test_stream_decode_codeword_incl_parity(oracle_mod, torch_cuda, auto_exec, cfg, sc):
+def test_stream_decode_codeword_incl_parity(oracle_mod, torch_cuda, stream_mode, cfg, sc):
     """Codewords with data AND parity erased: every rebuilt chunk (parity included) equals the
     encoded one; patterns with up to 4 erasures, one per y-section (the BASELINE worst case
     {0,4,8,12} first)."""
@@ -102,17 +119,17 @@ def test_stream_decode_codeword_incl_parity(oracle_mod, torch_cuda, auto_exec, c
     chunk = c.sub_chunk_no * sc
     ref = o.encode_array(np.random.default_rng(sc).integers(0, 256, c.k * chunk, dtype=np.uint8))
     pats = [[0, 4, 8, 12]] if cfg == (10, 4, 13) else [[0, 4, 8, 11]]
-    pats += [p for p in _patterns(c, 5, 12, 12) if stream_eligible(c, p)]
+    pats += [p for p in _patterns(c, 5, 12, 12) if stream_path(c, p)]
     for er in pats:
         got = _decode_dev(torch, c, ref, er, chunk)
-        assert clay_amd.last_exec_path() == auto_exec, er
+        assert clay_amd.last_exec_path() == stream_path(c, er), er
         for e in er:
             assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e)
 
 
-def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, auto_exec):
-    """Same random inputs through the streaming kernel (auto) and the grouped plan executor:
-    identical bytes, including the rebuilt parity chunk."""
+def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, stream_mode):
+    """Same random inputs through the streaming kernel and the grouped plan executor: identical
+    bytes, including the rebuilt parity chunk."""
     torch = torch_cuda
     c = ClayCode(10, 4, 13)
     sc = 64 * 50 + 8
@@ -120,7 +137,7 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, auto_exe
     chunks = np.random.default_rng(9).integers(0, 256, (c.n, chunk), dtype=np.uint8)
     er = [1, 6, 9, 13]
     a = _decode_dev(torch, c, chunks, er, chunk)
-    assert clay_amd.last_exec_path() == auto_exec
+    assert clay_amd.last_exec_path() == "stream-fused2"
     clay_amd.set_exec_mode("grouped")
     b = _decode_dev(torch, c, chunks, er, chunk)
     assert clay_amd.last_exec_path() == "grouped"
