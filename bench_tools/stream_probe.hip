@@ -55,12 +55,18 @@ static float run_b2b(BsArgs a, int n) {
     (void)hipEventSynchronize(e1);
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        printf("HIP error (probe %d): %s\n", PROBE, hipGetErrorString(err));
+        exit(3);
+    }
     return ms / float(n);
 }
 
 // Segment timing (PROBE 4096, stream_encode.hpp TimeAcc): per-workgroup s_memtime sums of the
 // last of `n` back-to-back launches, then one single launch timed with events to convert cycles
 // to time.  Prints per-tile averages over the workgroups and the start / end spread.
+template <int TP>
 static void timing_report(BsArgs a, int n) {
     using Kn = StreamEnc<10, 4>;
     const int grid = int(a.nslots) * 8;
@@ -69,27 +75,29 @@ static void timing_report(BsArgs a, int n) {
     (void)hipMemset(tb, 0, size_t(grid) * 80 * 8);
     a.par[4] = reinterpret_cast<uint8_t *>(tb);
     const float ms_plain = run_b2b<4, 0>(a, n);
-    const float ms_tm = run_b2b<4, 4096>(a, n);
+    const float ms_tm = run_b2b<4, TP>(a, n);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    k_stream_encode<10, 4, 4096><<<dim3(grid), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
+    k_stream_encode<10, 4, TP><<<dim3(grid), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms1;
     (void)hipEventElapsedTime(&ms1, e0, e1);
     std::vector<uint64_t> h(size_t(grid) * 80);
     (void)hipMemcpy(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost);
+    // s_memtime counts per XCD (the counters of different XCDs are not aligned): the spread is taken
+    // inside XCD 0 (workgroups b with b % 8 == 0)
     uint64_t t0 = ~0ull, t1 = 0;
-    for (int b = 0; b < grid; b++)
+    for (int b = 0; b < grid; b += 8)
         for (int r = 0; r < 3; r++) {
             const uint64_t *p = &h[size_t(b) * 80 + r * 24];
             t0 = std::min(t0, p[13]);
             t1 = std::max(t1, p[15]);
         }
     const double span = double(t1 - t0), ghz = span / (ms1 * 1e6);
-    printf("b2b ms: plain %.4f  timing-probe %.4f   single timed launch %.4f ms = %.0f cycles -> %.3f GHz\n",
+    printf("b2b ms: plain %.4f  timing-probe %.4f   single timed launch %.4f ms; XCD 0 span %.0f cycles -> %.3f GHz\n",
            ms_plain, ms_tm, ms1, span, ghz);
     const char *role[3] = {"compute wave 0", "compute wave 7", "loader wave 0"};
     const char *kinds[2][3] = {{"barrier wait", "section math", "-"}, {"vmcnt wait", "barrier", "DMA issue"}};
@@ -116,11 +124,11 @@ static void timing_report(BsArgs a, int n) {
         if (r < 2)
             printf("   end of group g0 %6.0f  g1 %6.0f  g2 %6.0f  g3 %6.0f   sum %6.0f\n", ge[0] / G, ge[1] / G, ge[2] / G,
                    ge[3] / G, (ge[0] + ge[1] + ge[2] + ge[3]) / G);
-        printf("   start -> first step %.0f cycles (avg)\n", first / G);
+        printf("   start -> loop %.0f cycles (avg)\n", first / G);
     }
-    // start / end spread of compute wave 0 over the workgroups
+    // start / end spread of compute wave 0 over the workgroups of XCD 0
     std::vector<double> st, en;
-    for (int b = 0; b < grid; b++) {
+    for (int b = 0; b < grid; b += 8) {
         const uint64_t *p = &h[size_t(b) * 80];
         st.push_back(double(p[13] - t0));
         en.push_back(double(p[15] - t0));
@@ -161,11 +169,50 @@ int main(int argc, char **argv) {
         printf("%-34s %8.4f ms  %7.1f GB/s (algorithmic)\n", n, ms, bytes / (ms * 1e-3) / 1e9);
         fflush(stdout);
     };
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_stream_encode<10, 2, 0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, StreamEnc<10, 2>::LDS_BYTES);
     for (int i = 0; i < 300; i++) k_stream_encode<10, 2, 0><<<dim3(a.nslots * 8), dim3(StreamEnc<10, 2>::BLOCK), StreamEnc<10, 2>::LDS_BYTES>>>(a);
-    (void)hipDeviceSynchronize();
+    {
+        const hipError_t e = hipDeviceSynchronize();
+        const hipError_t e2 = hipGetLastError();
+        if (e != hipSuccess || e2 != hipSuccess) {
+            printf("HIP error after warm-up: %s / %s\n", hipGetErrorString(e), hipGetErrorString(e2));
+            return 3;
+        }
+    }
     if (argc > 2 && argv[2][0] == 't') {  // segment timing of the full kernel
         printf("sc %u segment timing\n", sc);
-        for (int rr = 0; rr < 2; rr++) timing_report(a, 200);
+        timing_report<4096>(a, 200);
+        printf("---- deferred end of group (PROBE 8192)\n");
+        timing_report<4096 | 8192>(a, 200);
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'd') {  // deferred end-of-group work (PROBE 8192) A/B
+        printf("sc %u deferred end-of-group A/B, back-to-back\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b full", run_b2b<4, 0>(a, 200));
+            rep("b2b full, end of group after the next barrier", run_b2b<4, 8192>(a, 200));
+            rep("b2b memory only", run_b2b<4, 1>(a, 200));
+            rep("b2b memory only, deferred", run_b2b<4, 8193>(a, 200));
+            rep("b2b full, no sched barrier between nodes", run_b2b<4, 16384>(a, 200));
+            rep("b2b full, sched barrier every 2 nodes", run_b2b<4, 32768>(a, 200));
+            rep("b2b full, deferred + every 2 nodes", run_b2b<4, 32768 | 8192>(a, 200));
+        }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'v') {  // steady-state variants: which parts add
+        printf("sc %u variants, back-to-back (200 launches after 50 untimed)\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b full", run_b2b<4, 0>(a, 200));
+            rep("b2b no parity stores (math + DMA)", run_b2b<4, 4>(a, 200));
+            rep("b2b memory only (DMA + stores)", run_b2b<4, 1>(a, 200));
+            rep("b2b math + stores (no DMA)", run_b2b<4, 2>(a, 200));
+            rep("b2b math only", run_b2b<4, 6>(a, 200));
+            rep("b2b reads only", run_b2b<4, 5>(a, 200));
+            rep("b2b stores only", run_b2b<4, 3>(a, 200));
+            rep("b2b L0 full (compute waves issue the DMA)", run_b2b<0, 0>(a, 200));
+            rep("b2b L2 full", run_b2b<2, 0>(a, 200));
+        }
         return 0;
     }
     if (argc > 2 && argv[2][0] == 'l') {  // steady state: loader-wave count

@@ -285,8 +285,9 @@ struct StreamEnc {
     // One step: the 4 nodes of section Y (own + companion reads, PRT, transpose, RS fold),
     // each node's LDS reads issued one node ahead; the scheduling barrier after every node
     // keeps the compiler from hoisting more reads (register pressure: 3 waves per SIMD).
-    template <int Y>
-    __device__ static void section(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
+    // SBN (probe builds): a scheduling barrier after every SBN nodes (0: none)
+    template <int Y, int SBN = 1>
+    __device__ __forceinline__ static void section(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
         uint32_t o[2][8], cv[2][8];
         load_x<Y, 0>(slot, L, o[0], cv[0]);
         sfor<Q>([&](auto xc) BS_INL {
@@ -296,7 +297,7 @@ struct StreamEnc {
             prt_x<Y, x>(o[x & 1], cv[x & 1], L, u);
             if constexpr (CSE) K6::template fold_x_cse<Y, x>(u, acc);
             else K6::template fold_x<Y, x>(u, acc);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SBN > 0 && (x + 1) % SBN == 0) __builtin_amdgcn_sched_barrier(0);
         });
     }
 
@@ -306,7 +307,7 @@ struct StreamEnc {
     // halves by DPP so that each 16-byte store instruction of a wave writes 4 whole
     // 256-byte row runs (even columns, then odd columns) instead of 8 rows x 128 B.
     template <int X>
-    __device__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, StreamTile t, uint32_t prel,
+    __device__ __forceinline__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, StreamTile t, uint32_t prel,
                                bool ragged) {
         transpose8(cv);
         if (!ragged) {
@@ -322,8 +323,9 @@ struct StreamEnc {
             uint32_t off = (z - (odd ? 4u : 0u)) * uint32_t(a.sc);
             asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
             off += t.b0 + prel + (odd ? 128u : 0u);
-            st16sp<CPS>(a.par[X], off, lo[0], lo[1], lo[2], lo[3]);
-            st16sp<CPS>(a.par[X], off + 4u * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
+            const uint8_t *base = uniform_ptr(a.par[X]);  // SGPR base (also under the probes' deferred flow)
+            st16sp<CPS>(base, off, lo[0], lo[1], lo[2], lo[3]);
+            st16sp<CPS>(base, off + 4u * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
         } else {
             uint8_t *p = a.par[X] + uint64_t(z) * a.sc + t.b0 + prel;
 #pragma unroll
@@ -338,9 +340,10 @@ struct StreamEnc {
         }
     }
     // Group G finished: red vertex C[G][z_G] = U, and the PFT pairs with groups h < G
-    // (transforms.rs:108-125) (Hold: encode_math.hpp).
+    // (transforms.rs:108-125) (Hold: encode_math.hpp).  Force-inlined: called out of line
+    // (several instantiations in one translation unit), acc and Hold would go through scratch.
     template <int G>
-    __device__ static void end_group(const BsArgs &a, const uint32_t (&acc)[Q * 8], typename K6::Hold &H, int c,
+    __device__ __forceinline__ static void end_group(const BsArgs &a, const uint32_t (&acc)[Q * 8], typename K6::Hold &H, int c,
                                      StreamTile t, uint32_t prel, bool ragged) {
         const uint32_t zg = uint32_t(c * 4 + G);
         uint32_t cv[8];
@@ -404,7 +407,9 @@ struct StreamEnc {
 // (no CSE: bench_tools/stream_probe x, 0.350 vs 0.353 ms full, 0.257 vs 0.281 math + stores),
 // 8 = loaders at default priority, 16 = compute waves 4-7 at priority 1, 32 = the group whose
 // outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
-// across workgroups; only meaningful with bit 1), 2048 = chip round-robin tile map (ChipMap).
+// across workgroups; only meaningful with bit 1), 2048 = chip round-robin tile map (ChipMap),
+// 4096 = s_memtime segment timing (TimeAcc), 8192 = a group's end work after the next barrier,
+// 16384 / 32768 = no scheduling barrier between nodes / one after every two nodes.
 // Segment timing of the probe instantiations (PROBE bit 4096): s_memtime cycles summed per
 // kind (compute wave: 0 barrier wait, 1 section math; loader wave: 0 vmcnt wait, 1 barrier,
 // 2 DMA issue) and per section y, plus the end-of-group work (outputs) per group g; written by
@@ -471,10 +476,11 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         T.t_start = TM ? __builtin_amdgcn_s_memtime() : 0;
         if constexpr (!(PROBE & 2))
             for (int s = 0; s < 3 && s < nsteps; s++) Kn::issue_any(s % 3, a, L, lds0, tm.tile(0, slot, ns), s / 3);
+        uint64_t t0 = TM ? __builtin_amdgcn_s_memtime() : 0;  // chained: every cycle lands in one sum
+        if constexpr (TM) T.t_first = t0;
         for (int s = 0; s < nsteps; s++) {
             const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
             const StreamTile t = tm.tile(k, slot, ns);
-            uint64_t t0 = TM ? __builtin_amdgcn_s_memtime() : 0;
             // step s landed: everything issued after it may stay in flight
             int after = 0;
             if (s == 0) {
@@ -499,10 +505,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
                 const int k2 = s2 / Kn::STEPS, r2 = s2 % Kn::STEPS;
                 Kn::issue_any(r2 % 3, a, L, lds0, tm.tile(k2, slot, ns), r2 / 3);
             }
-            if constexpr (TM) {
-                T.add(2, y, t0);
-                if (s == 0) T.t_first = t0;
-            }
+            if constexpr (TM) T.add(2, y, t0);
         }
         if constexpr (TM) {
             T.t_end = __builtin_amdgcn_s_memtime();
@@ -530,11 +533,23 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             for (int s = 0; s < 3 && s < nsteps; s++) Kn::issue_any(s % 3, a, LD, lds0, tm.tile(0, slot, ns), s / 3);
     }
     int st1 = 0, st2 = 0;  // counted stores issued in steps s-1 and s-2
+    // PROBE 8192 (probe builds only): group g's end work deferred to after the next step's barrier
+    constexpr bool DEFER = (PROBE & 8192) != 0 && LOADERS > 0;
+    int pend = -1;
+    StreamTile pt{0, 0};
+    auto end_any = [&](int ge, StreamTile t) BS_INL {
+        const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
+        if (ge == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged);
+        else if (ge == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged);
+        else if (ge == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged);
+        else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged);
+    };
     TimeAcc T;
     T.t_start = TM ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t t0 = TM ? __builtin_amdgcn_s_memtime() : 0;  // chained: every cycle lands in one sum
+    if constexpr (TM) T.t_first = t0;
     for (int s = 0; s < nsteps; s++) {
         const int k = s / Kn::STEPS, r = s % Kn::STEPS, g = r / 3, y = r % 3;
-        uint64_t t0 = TM ? __builtin_amdgcn_s_memtime() : 0;
         if constexpr (LOADERS == 0 && !(PROBE & 2)) {
             const StreamTile t = tm.tile(k, slot, ns);
             int after;
@@ -549,9 +564,15 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             }
         }
         lds_barrier();
-        if constexpr (TM) {
-            T.add(0, y, t0);
-            if (s == 0) T.t_first = t0;
+        if constexpr (TM) T.add(0, y, t0);
+        if constexpr (DEFER) {
+            // the previous group's outputs (PFT, transposes, stores) after this step's barrier:
+            // the barrier, and with it the loaders' next DMA, no longer waits for them
+            if (pend >= 0) {
+                end_any(pend, pt);
+                if constexpr (TM) T.addg(pend, t0);
+                pend = -1;
+            }
         }
         if constexpr (LOADERS == 0 && !(PROBE & 2)) {
             const int s2 = s + 2;
@@ -572,19 +593,22 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
 #pragma unroll
                 for (int w = 0; w < Kn::Q * 8; w++) acc[w] = (threadIdx.x * 0x9E3779B9u) ^ uint32_t(w) ^ L.own[0];
         } else {
-            if (y == 0) Kn::template section<0>(smem, L, acc);
-            else if (y == 1) Kn::template section<1>(smem + Kn::REGION, L, acc);
-            else Kn::template section<2>(smem + 2 * Kn::REGION, L, acc);
+            constexpr int SBN = (PROBE & 16384) ? 0 : (PROBE & 32768) ? 2 : 1;
+            if (y == 0) Kn::template section<0, SBN>(smem, L, acc);
+            else if (y == 1) Kn::template section<1, SBN>(smem + Kn::REGION, L, acc);
+            else Kn::template section<2, SBN>(smem + 2 * Kn::REGION, L, acc);
         }
         if constexpr (TM) T.add(1, y, t0);
         if (y == 2 && !(PROBE & 4)) {
             const StreamTile t = tm.tile(k, slot, ns);
             const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
             const int ge = (PROBE & 32) ? ((g + int(slot)) & 3) : g;
-            if (ge == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged);
-            else if (ge == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged);
-            else if (ge == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged);
-            else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged);
+            if constexpr (DEFER) {
+                pend = ge;
+                pt = t;
+            } else {
+                end_any(ge, t);
+            }
             st2 = st1;
             st1 = ragged ? 0 : Kn::nstores(ge);  // a ragged tile's plain stores are not counted:
                                                  // the waits then cover more than needed
@@ -593,6 +617,9 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             st1 = 0;
         }
         if constexpr (TM) T.addg(g, t0);
+    }
+    if constexpr (DEFER) {
+        if (pend >= 0) end_any(pend, pt);
     }
     if constexpr (TM) {
         T.t_end = __builtin_amdgcn_s_memtime();

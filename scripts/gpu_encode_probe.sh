@@ -1,0 +1,12 @@
+#!/bin/bash
+# Encode segment timing + steady-state variants (bench_tools/stream_probe, built in-tree):
+#   t = s_memtime segment split per wave role, v = which parts of the kernel add.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$R" && mkdir -p gpurun_out
+TAG=${1:-probe}
+for m in ${MODES:-t v}; do
+  echo "[$(date +%T)] stream_probe $m"
+  timeout -k 10 240 ./bench_tools/stream_probe 419432 $m > gpurun_out/${TAG}_$m.txt 2>&1 || { echo "probe $m failed rc=$?"; tail -20 gpurun_out/${TAG}_$m.txt; exit 1; }
+  cat gpurun_out/${TAG}_$m.txt
+done

@@ -17,15 +17,17 @@ pytestmark = pytest.mark.gpu
 
 
 def _decode_dev(torch, c, full, er, chunk, codeword=True, stream=None):
-    outs = torch.full((c.n, chunk), 0xA5, dtype=torch.uint8, device="cuda")
-    sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
-    c.decode_device([None if i in er else full[i] for i in range(c.n)], er,
-                    [outs[i] if i in er else None for i in range(c.n)], chunk, 0, sh, codeword=codeword)
-    if stream is not None:
-        stream.synchronize()
-    else:
-        torch.cuda.synchronize()
-    return outs
+    """Output buffer fill, decode and read-back all on one stream (the thread's own in the
+    concurrency test), so nothing races with the fill."""
+    st = stream if stream is not None else torch.cuda.current_stream()
+    with torch.cuda.stream(st):
+        outs = torch.full((c.n, chunk), 0xA5, dtype=torch.uint8, device="cuda")
+        c.decode_device([None if i in er else full[i] for i in range(c.n)], er,
+                        [outs[i] if i in er else None for i in range(c.n)], chunk, 0, st.cuda_stream,
+                        codeword=codeword)
+        host = outs.cpu()
+    st.synchronize()
+    return host
 
 
 # sub-chunks that give every CU of a 256-CU MI355X at least one tile of the streaming repair
@@ -41,7 +43,7 @@ def test_codeword_single_erasure_runs_repair(oracle_mod, torch_cuda, cfg, sc, lo
     for e in lost:
         outs = _decode_dev(torch, c, full, [e], chunk)
         assert clay_amd.last_exec_path() == "bs-repair-stream", (e, clay_amd.last_exec_path())
-        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (cfg, e)
+        assert np.array_equal(outs[e].numpy(), ref[e]), (cfg, e)
         # the other outputs were not requested and stay untouched
         assert int((outs[(e + 1) % c.n] != 0xA5).sum().item()) == 0
 
@@ -58,7 +60,7 @@ def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda):
         outs = _decode_dev(torch, c, full, er, chunk)
         assert clay_amd.last_exec_path() == "stream-local", (sc, er, clay_amd.last_exec_path())
         for e in er:
-            assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (sc, er, e)
+            assert np.array_equal(outs[e].numpy(), ref[e]), (sc, er, e)
 
 
 def test_plain_decode_keeps_decode_semantics_on_non_codewords(oracle_mod, torch_cuda):
@@ -73,7 +75,7 @@ def test_plain_decode_keeps_decode_semantics_on_non_codewords(oracle_mod, torch_
     assert clay_amd.last_exec_path() == "stream-local"
     av = {i: chunks[i] for i in range(c.n) if i != 2}
     ref = np.frombuffer(o.decode(av, [2]), dtype=np.uint8).reshape(c.k, -1)
-    assert np.array_equal(outs[2].cpu().numpy(), ref[2])
+    assert np.array_equal(outs[2].numpy(), ref[2])
 
 
 def test_codeword_call_does_not_change_concurrent_decodes(oracle_mod, torch_cuda):
@@ -98,7 +100,7 @@ def test_codeword_call_does_not_change_concurrent_decodes(oracle_mod, torch_cuda
         for _ in range(12):
             out = _decode_dev(torch, c, cw, [2], chunk, codeword=True, stream=s)
             paths["a"].add(clay_amd.last_exec_path())
-            if not np.array_equal(out[2].cpu().numpy(), ref[2]):
+            if not np.array_equal(out[2].numpy(), ref[2]):
                 errors.append("codeword decode")
 
     def thread_b():
@@ -107,7 +109,7 @@ def test_codeword_call_does_not_change_concurrent_decodes(oracle_mod, torch_cuda
         for _ in range(12):
             out = _decode_dev(torch, c, rd, [2], chunk, codeword=False, stream=s)
             paths["b"].add(clay_amd.last_exec_path())
-            if not np.array_equal(out[2].cpu().numpy(), want_b):
+            if not np.array_equal(out[2].numpy(), want_b):
                 errors.append("plain decode of random chunks changed")
 
     ts = [threading.Thread(target=thread_a), threading.Thread(target=thread_b)]
