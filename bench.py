@@ -64,7 +64,7 @@ def parse(argv=None):
     ap.add_argument("--no-small", action="store_true", help="skip the clay_bench-size GPU batch rates")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the driver-timed legs of BASELINE configs 2, 3 and 5 (after the timed region)")
-    ap.add_argument("--leg-calls", type=int, default=20, help="timed calls per config leg")
+    ap.add_argument("--leg-calls", type=int, default=30, help="timed calls per config leg")
     ap.add_argument("--path", default="auto",
                     choices=["auto", "fused", "staged", "bitsliced", "stream"])
     ap.add_argument("--tile", type=int, default=0, help="encode path variant (clay_set_encode_path)")
@@ -292,7 +292,7 @@ def small_stripe_rates(torch, dev, local, sh):
     return out
 
 
-def _event_times(torch, stream, fn, calls: int, warm: int = 3):
+def _event_times(torch, stream, fn, calls: int, warm: int = 10):
     """HIP-event time of each of `calls` back-to-back calls on `stream` (events recorded on the
     launch stream, all calls queued before one synchronize), after `warm` untimed calls."""
     for _ in range(warm):
@@ -309,7 +309,8 @@ def _event_times(torch, stream, fn, calls: int, warm: int = 3):
 
 def _leg(name, ms, algo, path, verified, extra=None):
     mean = float(np.mean(ms))
-    d = {"workload": name, "kernel_ms_mean": round(mean, 4), "kernel_ms_min": round(float(min(ms)), 4),
+    d = {"workload": name, "kernel_ms_mean": round(mean, 4), "kernel_ms_median": round(float(np.median(ms)), 4),
+         "kernel_ms_min": round(float(min(ms)), 4),
          "calls": len(ms), "algorithmic_bytes": int(algo), "achieved_GBps": round(algo / (mean * 1e-3) / 1e9, 1),
          "frac": round(algo / (mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "path": path, "verified_vs_oracle": verified}
     if extra:

@@ -70,78 +70,38 @@ template <int TP>
 static void timing_report(BsArgs a, int n) {
     using Kn = StreamEnc<10, 4>;
     const int grid = int(a.nslots) * 8;
+    const size_t rec = size_t(grid) * 12 * 24;
     uint64_t *tb;
-    (void)hipMalloc(&tb, size_t(grid) * 80 * 8);
-    (void)hipMemset(tb, 0, size_t(grid) * 80 * 8);
+    (void)hipMalloc(&tb, rec * 8);
+    (void)hipMemset(tb, 0, rec * 8);
     a.par[4] = reinterpret_cast<uint8_t *>(tb);
     const float ms_plain = run_b2b<4, 0>(a, n);
     const float ms_tm = run_b2b<4, TP>(a, n);
-    hipEvent_t e0, e1;
-    (void)hipEventCreate(&e0);
-    (void)hipEventCreate(&e1);
-    (void)hipEventRecord(e0);
-    k_stream_encode<10, 4, TP><<<dim3(grid), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
-    (void)hipEventRecord(e1);
-    (void)hipEventSynchronize(e1);
-    float ms1;
-    (void)hipEventElapsedTime(&ms1, e0, e1);
-    std::vector<uint64_t> h(size_t(grid) * 80);
-    (void)hipMemcpy(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost);
-    // s_memtime counts per XCD (the counters of different XCDs are not aligned): the spread is taken
-    // inside XCD 0 (workgroups b with b % 8 == 0)
-    uint64_t t0 = ~0ull, t1 = 0;
-    for (int b = 0; b < grid; b += 8)
-        for (int r = 0; r < 3; r++) {
-            const uint64_t *p = &h[size_t(b) * 80 + r * 24];
-            t0 = std::min(t0, p[13]);
-            t1 = std::max(t1, p[15]);
-        }
-    const double span = double(t1 - t0), ghz = span / (ms1 * 1e6);
-    printf("b2b ms: plain %.4f  timing-probe %.4f   single timed launch %.4f ms; XCD 0 span %.0f cycles -> %.3f GHz\n",
-           ms_plain, ms_tm, ms1, span, ghz);
-    const char *role[3] = {"compute wave 0", "compute wave 7", "loader wave 0"};
-    const char *kinds[2][3] = {{"barrier wait", "section math", "-"}, {"vmcnt wait", "barrier", "DMA issue"}};
-    for (int r = 0; r < 3; r++) {
-        double v[3][3] = {}, ge[4] = {}, tiles = 0, first = 0, tot = 0;
+    std::vector<uint64_t> h(rec);
+    (void)hipMemcpy(h.data(), tb, rec * 8, hipMemcpyDeviceToHost);
+    printf("b2b ms: plain %.4f  timing-probe %.4f (s_memtime counts per XCD; cycles below are per tile)\n", ms_plain, ms_tm);
+    printf("wave  role     total   bar/vm y0   y1    y2 | math/bar y0   y1    y2 | issue y0  y1    y2 | end g0  g1    g2    g3\n");
+    for (int w = 0; w < 12; w++) {
+        double v[3][3] = {}, ge[4] = {}, tot = 0;
+        int cnt = 0;
         for (int b = 0; b < grid; b++) {
-            const uint64_t *p = &h[size_t(b) * 80 + r * 24];
+            const uint64_t *p = &h[(size_t(b) * 12 + w) * 24];
             const double nt = double(p[16]);
             if (nt == 0) continue;
+            cnt++;
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) v[i][j] += double(p[i * 3 + j]) / nt;
             for (int g = 0; g < 4; g++) ge[g] += double(p[9 + g]) / nt;
-            first += double(p[14] - p[13]);
             tot += double(p[15] - p[13]) / nt;
-            tiles += nt;
         }
-        const double G = grid;
-        printf("%s: per tile (avg over %d workgroups, %.2f tiles each): total %.0f cycles\n", role[r], grid, tiles / G,
-               tot / G);
-        const int nk = r < 2 ? 2 : 3;
-        for (int i = 0; i < nk; i++)
-            printf("   %-13s y0 %7.0f  y1 %7.0f  y2 %7.0f   sum %7.0f\n", kinds[r < 2 ? 0 : 1][i], v[i][0] / G, v[i][1] / G,
-                   v[i][2] / G, (v[i][0] + v[i][1] + v[i][2]) / G);
-        if (r < 2)
-            printf("   end of group g0 %6.0f  g1 %6.0f  g2 %6.0f  g3 %6.0f   sum %6.0f\n", ge[0] / G, ge[1] / G, ge[2] / G,
-                   ge[3] / G, (ge[0] + ge[1] + ge[2] + ge[3]) / G);
-        printf("   start -> loop %.0f cycles (avg)\n", first / G);
+        const double G = cnt ? cnt : 1;
+        printf("%4d  %-7s %7.0f  %6.0f %6.0f %6.0f | %6.0f %6.0f %6.0f | %6.0f %6.0f %6.0f | %5.0f %5.0f %5.0f %5.0f\n", w,
+               w < 8 ? "compute" : "loader", tot / G, v[0][0] / G, v[0][1] / G, v[0][2] / G, v[1][0] / G, v[1][1] / G,
+               v[1][2] / G, v[2][0] / G, v[2][1] / G, v[2][2] / G, ge[0] / G, ge[1] / G, ge[2] / G, ge[3] / G);
     }
-    // start / end spread of compute wave 0 over the workgroups of XCD 0
-    std::vector<double> st, en;
-    for (int b = 0; b < grid; b += 8) {
-        const uint64_t *p = &h[size_t(b) * 80];
-        st.push_back(double(p[13] - t0));
-        en.push_back(double(p[15] - t0));
-    }
-    std::sort(st.begin(), st.end());
-    std::sort(en.begin(), en.end());
-    auto pc = [](const std::vector<double> &v, double q) { return v[size_t(q * double(v.size() - 1))]; };
-    printf("workgroup start (cycles after the first): p0 %.0f p50 %.0f p90 %.0f p100 %.0f\n", pc(st, 0), pc(st, .5),
-           pc(st, .9), pc(st, 1));
-    printf("workgroup end   (cycles after the first start): p0 %.0f p10 %.0f p50 %.0f p90 %.0f p100 %.0f\n", pc(en, 0),
-           pc(en, .1), pc(en, .5), pc(en, .9), pc(en, 1));
     fflush(stdout);
     (void)hipFree(tb);
+    (void)Kn::BLOCK;
 }
 
 int main(int argc, char **argv) {
@@ -200,6 +160,17 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
+    if (argc > 2 && argv[2][0] == 'p') {  // balanced issue priority (PROBE 131072) A/B
+        printf("sc %u balanced priority A/B, back-to-back\n", sc);
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b full", run_b2b<4, 0>(a, 200));
+            rep("b2b full, balanced priority", run_b2b<4, 131072>(a, 200));
+            rep("b2b math + stores (no DMA)", run_b2b<4, 2>(a, 200));
+            rep("b2b math + stores (no DMA), balanced priority", run_b2b<4, 2 | 131072>(a, 200));
+        }
+        timing_report<4096 | 131072>(a, 200);
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'v') {  // steady-state variants: which parts add
         printf("sc %u variants, back-to-back (200 launches after 50 untimed)\n", sc);
         for (int rr = 0; rr < 3; rr++) {
@@ -212,6 +183,7 @@ int main(int argc, char **argv) {
             rep("b2b stores only", run_b2b<4, 3>(a, 200));
             rep("b2b L0 full (compute waves issue the DMA)", run_b2b<0, 0>(a, 200));
             rep("b2b L2 full", run_b2b<2, 0>(a, 200));
+            rep("b2b math + stores, no DMA, no barriers", run_b2b<4, 2 | 65536>(a, 200));
         }
         return 0;
     }

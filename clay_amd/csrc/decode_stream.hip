@@ -81,10 +81,17 @@ hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t
     // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only, 36 no rounds / presolve,
     // 37 no rounds / stores, 38 no rounds / phase-A math (presolve kept), 39 no presolve
     // 40: the full kernel with s_memtime segment timing (workgroup 0 prints its compute wave 0 and
-    // loader wave 0 totals)
-    if (kd == 10 && probe >= 31 && probe <= 40) {
+    // loader wave 0 totals); 41 / 42: the rounds at priority 0 (without / with the timing); 43 / 44:
+    // phase A with the {0,4,8,12} masks at compile time (only valid for that pattern)
+    if (kd == 10 && probe >= 31 && probe <= 46) {
         switch (probe) {
         case 40: return launch_f2<10, 16>(a, stream, dev);
+        case 41: return launch_f2<10, 64>(a, stream, dev);
+        case 42: return launch_f2<10, 64 | 16>(a, stream, dev);
+        case 43: return launch_f2<10, 128>(a, stream, dev);
+        case 44: return launch_f2<10, 128 | 16>(a, stream, dev);
+        case 45: return launch_f2<10, 256>(a, stream, dev);
+        case 46: return launch_f2<10, 256 | 16>(a, stream, dev);
         case 31: return launch_f2<10, 1>(a, stream, dev);
         case 32: return launch_f2<10, 2>(a, stream, dev);
         case 34: return launch_f2<10, 4>(a, stream, dev);

@@ -213,8 +213,12 @@ struct StreamDec {
                 lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
             }
             if constexpr ((PROBE & 2) != 0) return;
+            // PROBE 128 (probe library only): the (10,4,13) {0,4,8,12} pattern's masks as compile-time
+            // constants (alive / used / erased) -- measures what the run-time branches cost
+            constexpr bool K5 = (PROBE & 128) != 0;
+            constexpr uint32_t kAlive = 0xB2EEu, kUsed = 0xBEEEu, kEm[4] = {1u, 1u, 1u, 4u};
             const uint32_t c = opq(c0), poff = opq(poff0);
-            const uint32_t aliveY = (a.alive >> (4 * Y)) & 15u;
+            const uint32_t aliveY = K5 ? ((kAlive >> (4 * Y)) & 15u) : ((a.alive >> (4 * Y)) & 15u);
             const uint32_t rs = a.sec_off[Y];
             auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
                 const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
@@ -229,8 +233,8 @@ struct StreamDec {
                     constexpr int X = decltype(xc)::value;
                     constexpr int I = 4 * Y + X;
                     const bool alive_i = (aliveY >> X) & 1u;
-                    const bool used_i = (a.used >> I) & 1u;
-                    const bool erased_i = (a.emask[Y] >> X) & 1u;
+                    const bool used_i = K5 ? ((kUsed >> I) & 1u) : ((a.used >> I) & 1u);
+                    const bool erased_i = K5 ? ((kEm[Y] >> X) & 1u) : ((a.emask[Y] >> X) & 1u);
                     if (!(used_i || erased_i)) return;
                     uint32_t o[8], cv[8], u[8];
                     if (alive_i) {
@@ -287,7 +291,112 @@ struct StreamDec {
                         fold<4 * G + A, false>(v, S);
                         if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
                     });
-                } else if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
+                } else if ((K5 ? 2 : xeG) >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
+                    const int xe = K5 ? 2 : xeG;
+                    uint32_t v[8];
+                    sfor<4>([&](auto gc) BS_INL {
+                        constexpr int g = decltype(gc)::value;
+                        v[2 * g] = v[2 * g + 1] = 0;
+                        sfor<4>([&](auto ac) BS_INL {
+                            constexpr int A = decltype(ac)::value;
+                            if (A != g && xe == A) {
+                                v[2 * g] = gf_xt(o[g][2 * A]);
+                                v[2 * g + 1] = gf_xt(o[g][2 * A + 1]);
+                            }
+                        });
+                    });
+                    transpose8(v);
+                    sfor<4>([&](auto ac) BS_INL {  // S += H_eG Out(e_G, .)
+                        constexpr int A = decltype(ac)::value;
+                        if (A == xe) fold<4 * G + A, false>(v, S);
+                    });
+                }
+                sfor<4>([&](auto ac) BS_INL {
+                    constexpr int A = decltype(ac)::value;
+                    constexpr int I = 4 * G + A;
+                    if (!(K5 ? ((kUsed >> I) & 1u) : ((a.used >> I) & 1u))) return;
+                    uint32_t u[8];
+                    sfor<4>([&](auto gc) BS_INL {
+                        constexpr int g = decltype(gc)::value;
+                        const uint32_t keep = (A != g && ((aliveY >> g) & 1u)) ? 0xffffffffu : 0u;
+                        const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                        u[2 * g] = xor_xtime4_masked(o[A][2 * g], o[g][2 * A], ks, kr);
+                        u[2 * g + 1] = xor_xtime4_masked(o[A][2 * g + 1], o[g][2 * A + 1], ks, kr);
+                    });
+                    transpose8(u);
+                    fold<I, false>(u, S);
+                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+                });
+            }
+        });
+
+    }
+
+    // ---------------- phase A, branch-free (k_stream_fused2) ----------------
+    // The same sums as phase_a<.., RT = false> for at most one erasure per section, with the run-time
+    // pattern (alive / used / erased nodes) applied as lane masks instead of uniform branches, so
+    // every section is one straight-line block of four PRT + transpose + fold steps (the encode's
+    // shape): node X contributes H_X * U'(X), U'(X) = (own & m_own) + gamma * companion & keep, where
+    // m_own = "X alive and used" and keep = "companion real, not the red vertex, and X used or
+    // erased"; an erased node's U' is its Out term (own masked off), an ignored node's is 0.
+    // Section G keeps phase_a's form (one erased node at most: its Out fold, then the used nodes).
+    __device__ static uint32_t bmask(uint32_t bits, uint32_t i) { return ((bits >> i) & 1u) ? 0xffffffffu : 0u; }
+    __device__ static void phase_a_bf(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0,
+                                      int xeG, uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {
+        sfor<4>([&](auto yc) BS_INL {
+            constexpr int Y = decltype(yc)::value;
+            if (tbar) {
+                const uint64_t t0 = __builtin_amdgcn_s_memtime();
+                lds_barrier();
+                *tbar += __builtin_amdgcn_s_memtime() - t0;
+            } else {
+                lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
+            }
+            const uint32_t c = opq(c0), poff = opq(poff0);
+            // wave-uniform, opaque per step: the masks derived from them are not hoisted out of the
+            // tile loop into long-lived registers
+            uint32_t aliveY = __builtin_amdgcn_readfirstlane((a.alive >> (4 * Y)) & 15u);
+            uint32_t usedY = __builtin_amdgcn_readfirstlane((a.used >> (4 * Y)) & 15u);
+            uint32_t contribY = __builtin_amdgcn_readfirstlane(((a.used >> (4 * Y)) | a.emask[Y]) & 15u);
+            asm volatile("" : "+s"(aliveY), "+s"(usedY), "+s"(contribY));
+            const uint32_t rs = a.sec_off[Y];
+            auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive), else any buffer
+                const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
+                return ((aliveY >> x) & 1u) ? smem + ((qbase + q) % R) * BUF : smem;
+            };
+            if constexpr (Y != G) {
+                constexpr uint32_t sh = uint32_t(csh(Y));
+                const uint32_t cy = (c >> sh) & 3u;
+                const uint32_t comp_ok = bmask(aliveY, cy);  // per lane
+                const uint8_t *cbuf = buf_of(cy);            // per lane
+                sfor<4>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    constexpr int I = 4 * Y + X;
+                    const uint32_t m_own = bmask(aliveY & usedY, X);
+                    const uint32_t keep = comp_ok & bmask(contribY, X) & (cy != uint32_t(X) ? 0xffffffffu : 0u);
+                    const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                    uint32_t o[8], cv[8], u[8];
+                    read4(buf_of(X), c, poff, o);
+                    read4(cbuf, (c & ~(3u << sh)) | (uint32_t(X) << sh), poff, cv);
+#pragma unroll
+                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w] & m_own, cv[w], ks, kr);
+                    transpose8(u);
+                    fold<I, false>(u, S);
+                    __builtin_amdgcn_sched_barrier(0);  // one node's values live at a time
+                });
+            } else {
+                // section G as phase_a: per-node uniform branches (used / the one erased node)
+                uint32_t o[4][8];
+                sfor<4>([&](auto xc) BS_INL {
+                    constexpr int X = decltype(xc)::value;
+                    if ((aliveY >> X) & 1u) {
+                        read4(buf_of(X), c, poff, o[X]);
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < 8; w++) o[X][w] = 0;
+                    }
+                });
+                if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
                     uint32_t v[8];
                     sfor<4>([&](auto gc) BS_INL {
                         constexpr int g = decltype(gc)::value;
@@ -309,7 +418,7 @@ struct StreamDec {
                 sfor<4>([&](auto ac) BS_INL {
                     constexpr int A = decltype(ac)::value;
                     constexpr int I = 4 * G + A;
-                    if (!((a.used >> I) & 1u)) return;
+                    if (!((usedY >> A) & 1u)) return;
                     uint32_t u[8];
                     sfor<4>([&](auto gc) BS_INL {
                         constexpr int g = decltype(gc)::value;
@@ -320,11 +429,9 @@ struct StreamDec {
                     });
                     transpose8(u);
                     fold<I, false>(u, S);
-                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
                 });
             }
         });
-
     }
 
     // v_perm table i of a table block (8 dwords each, 5 used; decode_args.hpp)

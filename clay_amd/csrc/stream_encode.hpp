@@ -285,13 +285,17 @@ struct StreamEnc {
     // One step: the 4 nodes of section Y (own + companion reads, PRT, transpose, RS fold),
     // each node's LDS reads issued one node ahead; the scheduling barrier after every node
     // keeps the compiler from hoisting more reads (register pressure: 3 waves per SIMD).
-    // SBN (probe builds): a scheduling barrier after every SBN nodes (0: none)
-    template <int Y, int SBN = 1>
+    // SBN (probe builds): a scheduling barrier after every SBN nodes (0: none); BAL (probe
+    // builds): issue priority 1 for the first half of the section and 0 for the second, so the
+    // older of two compute waves on a SIMD yields to the younger once it is ahead
+    template <int Y, int SBN = 1, bool BAL = false>
     __device__ __forceinline__ static void section(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
         uint32_t o[2][8], cv[2][8];
+        if constexpr (BAL) __builtin_amdgcn_s_setprio(1);
         load_x<Y, 0>(slot, L, o[0], cv[0]);
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
+            if constexpr (BAL && x == 2) __builtin_amdgcn_s_setprio(0);
             if constexpr (x + 1 < Q) load_x<Y, x + 1>(slot, L, o[(x + 1) & 1], cv[(x + 1) & 1]);
             uint32_t u[8];
             prt_x<Y, x>(o[x & 1], cv[x & 1], L, u);
@@ -413,8 +417,7 @@ struct StreamEnc {
 // Segment timing of the probe instantiations (PROBE bit 4096): s_memtime cycles summed per
 // kind (compute wave: 0 barrier wait, 1 section math; loader wave: 0 vmcnt wait, 1 barrier,
 // 2 DMA issue) and per section y, plus the end-of-group work (outputs) per group g; written by
-// lane 0 of compute waves 0 and 7 and of loader wave 0 to a.par[4] (80 uint64 per workgroup:
-// records of 17 at 0, 24 and 48).
+// lane 0 of every wave to a.par[4] (a record of 17 uint64 at (workgroup * 12 + wave) * 24).
 struct TimeAcc {
     uint64_t v[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, gend[4] = {0, 0, 0, 0};
     uint64_t t_start = 0, t_first = 0, t_end = 0;
@@ -497,7 +500,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
                 wait_vm_rt(after);
             }
             if constexpr (TM) T.add(0, y, t0);
-            lds_barrier();
+            if constexpr (!(PROBE & 65536)) lds_barrier();
             if constexpr (TM) T.add(1, y, t0);
             // step s-1's buffers are free: refill them with step s+2
             const int s2 = s + 2;
@@ -509,7 +512,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         }
         if constexpr (TM) {
             T.t_end = __builtin_amdgcn_s_memtime();
-            if (lane == 0 && wave == Kn::CWAVES) T.put(reinterpret_cast<uint64_t *>(a.par[4]) + blockIdx.x * 80u + 48u, ntile);
+            if (lane == 0) T.put(reinterpret_cast<uint64_t *>(a.par[4]) + (blockIdx.x * 12u + uint32_t(wave)) * 24u, ntile);
         }
         return;
     }
@@ -563,7 +566,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
                 wait_vm_rt(after);
             }
         }
-        lds_barrier();
+        if constexpr (!(PROBE & 65536)) lds_barrier();  // 65536 (probe, with 2 only): no step barriers
         if constexpr (TM) T.add(0, y, t0);
         if constexpr (DEFER) {
             // the previous group's outputs (PFT, transposes, stores) after this step's barrier:
@@ -594,9 +597,10 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
                 for (int w = 0; w < Kn::Q * 8; w++) acc[w] = (threadIdx.x * 0x9E3779B9u) ^ uint32_t(w) ^ L.own[0];
         } else {
             constexpr int SBN = (PROBE & 16384) ? 0 : (PROBE & 32768) ? 2 : 1;
-            if (y == 0) Kn::template section<0, SBN>(smem, L, acc);
-            else if (y == 1) Kn::template section<1, SBN>(smem + Kn::REGION, L, acc);
-            else Kn::template section<2, SBN>(smem + 2 * Kn::REGION, L, acc);
+            constexpr bool BAL = (PROBE & 131072) != 0;
+            if (y == 0) Kn::template section<0, SBN, BAL>(smem, L, acc);
+            else if (y == 1) Kn::template section<1, SBN, BAL>(smem + Kn::REGION, L, acc);
+            else Kn::template section<2, SBN, BAL>(smem + 2 * Kn::REGION, L, acc);
         }
         if constexpr (TM) T.add(1, y, t0);
         if (y == 2 && !(PROBE & 4)) {
@@ -623,8 +627,7 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
     }
     if constexpr (TM) {
         T.t_end = __builtin_amdgcn_s_memtime();
-        if (lane == 0 && (wave == 0 || wave == Kn::CWAVES - 1))
-            T.put(reinterpret_cast<uint64_t *>(a.par[4]) + blockIdx.x * 80u + (wave == 0 ? 0u : 24u), ntile);
+        if (lane == 0) T.put(reinterpret_cast<uint64_t *>(a.par[4]) + (blockIdx.x * 12u + uint32_t(wave)) * 24u, ntile);
     }
 }
 

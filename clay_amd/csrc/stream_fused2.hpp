@@ -40,7 +40,8 @@ constexpr int kF2Items = 13;
 
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
 // 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
-// (workgroup 0 prints the totals of compute wave 0 and loader wave 0)
+// (workgroup 0 prints the totals of compute wave 0 and loader wave 0), 64 = rounds at priority 0,
+// 128 = phase A with the (10,4,13) {0,4,8,12} masks at compile time
 template <int KD, int G, int PROBE = 0>
 __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(DecArgs a) {
     using Kn = StreamDec<KD, G>;
@@ -187,6 +188,8 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 }
                 if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
                 if (k == 0 || (PROBE & 1)) return;
+                // PROBE 64: the round at the compute waves' priority (the DMA issue above stays at 3)
+                if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(0);
                 // ---- round of iscore level y + 1 of tile k - 1: every target layer z of the level
                 // red in section Y adds sum over X != x_e(Y) of A_(Y,X) C(e_Y, z[Y := X]) (the three
                 // terms summed in registers, one 64-bit LDS atomic per row)
@@ -214,6 +217,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                                                    uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(3);
                 if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
             });
             if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
@@ -250,8 +254,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
-            Kn::template phase_a<(PROBE & 4) ? 2 : 0, false, false>(a, smem, k * NT, c0, poff0, xeG, S, RB,
-                                                                    TM ? &tm_pabar : nullptr);
+            if constexpr ((PROBE & 256) != 0)  // probe: the branch-free phase A
+                Kn::phase_a_bf(a, smem, k * NT, c0, poff0, xeG, S, RB, TM ? &tm_pabar : nullptr);
+            else
+                Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false>(a, smem, k * NT, c0, poff0, xeG, S,
+                                                                                        RB, TM ? &tm_pabar : nullptr);
             // bit planes -> bytes
 #pragma unroll
             for (int j = 0; j < 4; j++) {
