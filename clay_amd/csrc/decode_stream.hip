@@ -82,16 +82,14 @@ hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t
     // 37 no rounds / stores, 38 no rounds / phase-A math (presolve kept), 39 no presolve
     // 40: the full kernel with s_memtime segment timing (workgroup 0 prints its compute wave 0 and
     // loader wave 0 totals); 41 / 42: the rounds at priority 0 (without / with the timing); 43 / 44:
-    // phase A with the {0,4,8,12} masks at compile time (only valid for that pattern)
-    if (kd == 10 && probe >= 31 && probe <= 46) {
+    // phase A without the per-section compile-time copies (without / with the timing)
+    if (kd == 10 && probe >= 31 && probe <= 44) {
         switch (probe) {
         case 40: return launch_f2<10, 16>(a, stream, dev);
         case 41: return launch_f2<10, 64>(a, stream, dev);
         case 42: return launch_f2<10, 64 | 16>(a, stream, dev);
         case 43: return launch_f2<10, 128>(a, stream, dev);
         case 44: return launch_f2<10, 128 | 16>(a, stream, dev);
-        case 45: return launch_f2<10, 256>(a, stream, dev);
-        case 46: return launch_f2<10, 256 | 16>(a, stream, dev);
         case 31: return launch_f2<10, 1>(a, stream, dev);
         case 32: return launch_f2<10, 2>(a, stream, dev);
         case 34: return launch_f2<10, 4>(a, stream, dev);

@@ -1835,6 +1835,16 @@ static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const 
     }
     a.sec_off[4] = nt;
     a.nt = nt;
+    // k_stream_fused2's compile-time phase-A copies: section y with at most one erased node x,
+    // every other node used and every node alive but that one and the shortened ones (i in [KD, 12))
+    for (int y = 0; y < 4; y++) {
+        uint32_t shortn = 0;
+        for (int x = 0; x < 4; x++)
+            if (4 * y + x >= KD && 4 * y + x < S::K) shortn |= 1u << x;
+        const uint32_t em = a.emask[y], un = (used >> (4 * y)) & 15u, al = (a.alive >> (4 * y)) & 15u;
+        const bool ok1 = __builtin_popcount(em) <= 1 && un == (~em & 15u) && al == (~em & ~shortn & 15u);
+        a.scase[y] = ok1 ? (em ? __builtin_ctz(em) : 4) : -1;
+    }
     if (nt == 0) return Error{};
     // the local kernel streams through R - 1 buffers (the last holds tables): a step's
     // loads are issued during the step before it, across tiles too (section 3 -> section 0)

@@ -200,9 +200,16 @@ struct StreamDec {
     // RT (k_stream_local): column digits at a.csh[y], and any number of erased nodes in section G
     // tbar (timing probe of k_stream_fused2 only): cycles spent in the four step barriers
     // SB: a scheduling barrier after every node's fold (one node's values live at a time)
+    //
+    // k_stream_fused2 (RT = false) dispatches each step on a.scase[Y] (engine.hip dec_setup): the
+    // section's erased node XE (4: none) when every other node of the section is used, so the
+    // step runs a copy with the section's structure (alive / used / erased) at compile time --
+    // straight-line PRT + fold code without the per-node branches, which the scheduler interleaves
+    // across nodes; -1 (an ignored node in the section: fewer than 4 erasures) takes the run-time
+    // copy.  PROBE 128 (probe library): always the run-time copy.
     template <int PROBE, bool RT = false, bool SB = true>
-    __device__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
-                                   uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {  // R: ring depth
+    __device__ __forceinline__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
+                                   uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {
         sfor<4>([&](auto yc) BS_INL {
             constexpr int Y = decltype(yc)::value;
             if (tbar) {
@@ -213,225 +220,156 @@ struct StreamDec {
                 lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
             }
             if constexpr ((PROBE & 2) != 0) return;
-            // PROBE 128 (probe library only): the (10,4,13) {0,4,8,12} pattern's masks as compile-time
-            // constants (alive / used / erased) -- measures what the run-time branches cost
-            constexpr bool K5 = (PROBE & 128) != 0;
-            constexpr uint32_t kAlive = 0xB2EEu, kUsed = 0xBEEEu, kEm[4] = {1u, 1u, 1u, 4u};
-            const uint32_t c = opq(c0), poff = opq(poff0);
-            const uint32_t aliveY = K5 ? ((kAlive >> (4 * Y)) & 15u) : ((a.alive >> (4 * Y)) & 15u);
-            const uint32_t rs = a.sec_off[Y];
-            auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
-                const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
-                return smem + ((qbase + q) % R) * BUF;
-            };
-            if constexpr (Y != G) {
-                const uint32_t sh = RT ? a.csh[Y] : uint32_t(csh(Y));
-                const uint32_t cy = (c >> sh) & 3u;
-                const bool comp_alive = (aliveY >> cy) & 1u;
-                const uint8_t *cbuf = comp_alive ? buf_of(cy) : smem;
-                sfor<4>([&](auto xc) BS_INL {
-                    constexpr int X = decltype(xc)::value;
-                    constexpr int I = 4 * Y + X;
-                    const bool alive_i = (aliveY >> X) & 1u;
-                    const bool used_i = K5 ? ((kUsed >> I) & 1u) : ((a.used >> I) & 1u);
-                    const bool erased_i = K5 ? ((kEm[Y] >> X) & 1u) : ((a.emask[Y] >> X) & 1u);
-                    if (!(used_i || erased_i)) return;
-                    uint32_t o[8], cv[8], u[8];
-                    if (alive_i) {
-                        read4(buf_of(X), c, poff, o);
-                    } else {
-#pragma unroll
-                        for (int w = 0; w < 8; w++) o[w] = 0;
-                    }
-                    const uint32_t cc = (c & ~(3u << sh)) | (uint32_t(X) << sh);
-                    read4(cbuf, cc, poff, cv);
-                    const uint32_t keep = (comp_alive && cy != uint32_t(X)) ? 0xffffffffu : 0u;
-                    const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
-                    if (erased_i) {  // S += H_e Out(e, z): Out = gamma * companion (0 where red)
-                        uint32_t v[8];
-#pragma unroll
-                        for (int w = 0; w < 8; w++) v[w] = xor_xtime4_masked(0u, cv[w], ks, kr);
-                        transpose8(v);
-                        fold<I, false>(v, S);
-                    }
-                    if (used_i) {
-#pragma unroll
-                        for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
-                        transpose8(u);
-                        fold<I, false>(u, S);
-                    }
-                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
-                });
-            } else {
-                // section G: all four nodes' slots are in the lane; U(a, g) = C(a, g) + gamma C(g, a)
-                uint32_t o[4][8];
-                sfor<4>([&](auto xc) BS_INL {
-                    constexpr int X = decltype(xc)::value;
-                    if ((aliveY >> X) & 1u) {
-                        read4(buf_of(X), c, poff, o[X]);
-                    } else {
-#pragma unroll
-                        for (int w = 0; w < 8; w++) o[X][w] = 0;
-                    }
-                });
-                if constexpr (RT) {
-                    // every erased node (G, A): Out((G, A), slot g) = gamma * C((G, g), slot A), 0 at
-                    // slot A and where (G, g) has no data (erased: a both-erased pair, inverted later)
-                    const uint32_t emG = a.emask[G];
-                    sfor<4>([&](auto ac) BS_INL {
-                        constexpr int A = decltype(ac)::value;
-                        if (!((emG >> A) & 1u)) return;
-                        uint32_t v[8];
-#pragma unroll
-                        for (int g = 0; g < 4; g++) {
-                            v[2 * g] = g == A ? 0u : gf_xt(o[g][2 * A]);
-                            v[2 * g + 1] = g == A ? 0u : gf_xt(o[g][2 * A + 1]);
-                        }
-                        transpose8(v);
-                        fold<4 * G + A, false>(v, S);
-                        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
-                    });
-                } else if ((K5 ? 2 : xeG) >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
-                    const int xe = K5 ? 2 : xeG;
-                    uint32_t v[8];
-                    sfor<4>([&](auto gc) BS_INL {
-                        constexpr int g = decltype(gc)::value;
-                        v[2 * g] = v[2 * g + 1] = 0;
-                        sfor<4>([&](auto ac) BS_INL {
-                            constexpr int A = decltype(ac)::value;
-                            if (A != g && xe == A) {
-                                v[2 * g] = gf_xt(o[g][2 * A]);
-                                v[2 * g + 1] = gf_xt(o[g][2 * A + 1]);
-                            }
-                        });
-                    });
-                    transpose8(v);
-                    sfor<4>([&](auto ac) BS_INL {  // S += H_eG Out(e_G, .)
-                        constexpr int A = decltype(ac)::value;
-                        if (A == xe) fold<4 * G + A, false>(v, S);
-                    });
+            if constexpr (!RT && (PROBE & 128) == 0) {
+                switch (a.scase[Y]) {
+                case 0: section<Y, 0, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 1: section<Y, 1, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 2: section<Y, 2, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 3: section<Y, 3, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 4: section<Y, 4, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                default: section<Y, -1, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
                 }
-                sfor<4>([&](auto ac) BS_INL {
-                    constexpr int A = decltype(ac)::value;
-                    constexpr int I = 4 * G + A;
-                    if (!(K5 ? ((kUsed >> I) & 1u) : ((a.used >> I) & 1u))) return;
-                    uint32_t u[8];
-                    sfor<4>([&](auto gc) BS_INL {
-                        constexpr int g = decltype(gc)::value;
-                        const uint32_t keep = (A != g && ((aliveY >> g) & 1u)) ? 0xffffffffu : 0u;
-                        const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
-                        u[2 * g] = xor_xtime4_masked(o[A][2 * g], o[g][2 * A], ks, kr);
-                        u[2 * g + 1] = xor_xtime4_masked(o[A][2 * g + 1], o[g][2 * A + 1], ks, kr);
-                    });
-                    transpose8(u);
-                    fold<I, false>(u, S);
-                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
-                });
+            } else {
+                section<Y, -1, RT, SB>(a, smem, qbase, c0, poff0, xeG, S, R);
             }
         });
-
     }
 
-    // ---------------- phase A, branch-free (k_stream_fused2) ----------------
-    // The same sums as phase_a<.., RT = false> for at most one erasure per section, with the run-time
-    // pattern (alive / used / erased nodes) applied as lane masks instead of uniform branches, so
-    // every section is one straight-line block of four PRT + transpose + fold steps (the encode's
-    // shape): node X contributes H_X * U'(X), U'(X) = (own & m_own) + gamma * companion & keep, where
-    // m_own = "X alive and used" and keep = "companion real, not the red vertex, and X used or
-    // erased"; an erased node's U' is its Out term (own masked off), an ignored node's is 0.
-    // Section G keeps phase_a's form (one erased node at most: its Out fold, then the used nodes).
-    __device__ static uint32_t bmask(uint32_t bits, uint32_t i) { return ((bits >> i) & 1u) ? 0xffffffffu : 0u; }
-    __device__ static void phase_a_bf(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0,
-                                      int xeG, uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {
-        sfor<4>([&](auto yc) BS_INL {
-            constexpr int Y = decltype(yc)::value;
-            if (tbar) {
-                const uint64_t t0 = __builtin_amdgcn_s_memtime();
-                lds_barrier();
-                *tbar += __builtin_amdgcn_s_memtime() - t0;
-            } else {
-                lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
-            }
-            const uint32_t c = opq(c0), poff = opq(poff0);
-            // wave-uniform, opaque per step: the masks derived from them are not hoisted out of the
-            // tile loop into long-lived registers
-            uint32_t aliveY = __builtin_amdgcn_readfirstlane((a.alive >> (4 * Y)) & 15u);
-            uint32_t usedY = __builtin_amdgcn_readfirstlane((a.used >> (4 * Y)) & 15u);
-            uint32_t contribY = __builtin_amdgcn_readfirstlane(((a.used >> (4 * Y)) | a.emask[Y]) & 15u);
-            asm volatile("" : "+s"(aliveY), "+s"(usedY), "+s"(contribY));
-            const uint32_t rs = a.sec_off[Y];
-            auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive), else any buffer
-                const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
-                return ((aliveY >> x) & 1u) ? smem + ((qbase + q) % R) * BUF : smem;
-            };
-            if constexpr (Y != G) {
-                constexpr uint32_t sh = uint32_t(csh(Y));
-                const uint32_t cy = (c >> sh) & 3u;
-                const uint32_t comp_ok = bmask(aliveY, cy);  // per lane
-                const uint8_t *cbuf = buf_of(cy);            // per lane
-                sfor<4>([&](auto xc) BS_INL {
-                    constexpr int X = decltype(xc)::value;
-                    constexpr int I = 4 * Y + X;
-                    const uint32_t m_own = bmask(aliveY & usedY, X);
-                    const uint32_t keep = comp_ok & bmask(contribY, X) & (cy != uint32_t(X) ? 0xffffffffu : 0u);
-                    const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
-                    uint32_t o[8], cv[8], u[8];
+    // shortened internal nodes of section y (i in [KD, 12): zero data, never loaded, always used)
+    static constexpr uint32_t short_nib(int y) {
+        uint32_t m = 0;
+        for (int x = 0; x < 4; x++)
+            if (4 * y + x >= KD && 4 * y + x < S::K) m |= 1u << x;
+        return m;
+    }
+
+    // one step of phase A.  XE >= 0: the compile-time structure of scase XE (node (Y, XE) erased,
+    // XE = 4: none; every other node used); XE = -1: the pattern's masks at run time
+    template <int Y, int XE, bool RT, bool SB>
+    __device__ __forceinline__ static void section(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0,
+                                   int xeG, uint32_t (&S)[32], uint32_t R) {
+        constexpr bool CT = XE >= 0;
+        constexpr uint32_t kEm = (CT && XE < 4) ? 1u << XE : 0u;
+        constexpr uint32_t kAlive = 15u & ~short_nib(Y) & ~kEm;
+        const uint32_t c = opq(c0), poff = opq(poff0);
+        // the run-time copy's masks, opaque per step: the branch conditions derived from them are
+        // not hoisted out of the tile loop into long-lived (spilled) scalar registers
+        uint32_t alive_all = __builtin_amdgcn_readfirstlane(a.alive), used_all = __builtin_amdgcn_readfirstlane(a.used),
+                 emY = __builtin_amdgcn_readfirstlane(a.emask[Y]);
+        if constexpr (!CT && !RT) asm volatile("" : "+s"(alive_all), "+s"(used_all), "+s"(emY));
+        const uint32_t aliveY = CT ? kAlive : ((alive_all >> (4 * Y)) & 15u);
+        const uint32_t rs = a.sec_off[Y];
+        auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
+            const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
+            return smem + ((qbase + q) % R) * BUF;
+        };
+        if constexpr (Y != G) {
+            const uint32_t sh = RT ? a.csh[Y] : uint32_t(csh(Y));
+            const uint32_t cy = (c >> sh) & 3u;
+            const bool comp_alive = (aliveY >> cy) & 1u;
+            const uint8_t *cbuf = comp_alive ? buf_of(cy) : smem;
+            sfor<4>([&](auto xc) BS_INL {
+                constexpr int X = decltype(xc)::value;
+                constexpr int I = 4 * Y + X;
+                const bool alive_i = (aliveY >> X) & 1u;
+                const bool used_i = CT ? X != XE : ((used_all >> I) & 1u);
+                const bool erased_i = CT ? X == XE : ((emY >> X) & 1u);
+                if (!(used_i || erased_i)) return;
+                uint32_t o[8], cv[8], u[8];
+                if (alive_i) {
                     read4(buf_of(X), c, poff, o);
-                    read4(cbuf, (c & ~(3u << sh)) | (uint32_t(X) << sh), poff, cv);
+                } else {
 #pragma unroll
-                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w] & m_own, cv[w], ks, kr);
+                    for (int w = 0; w < 8; w++) o[w] = 0;
+                }
+                const uint32_t cc = (c & ~(3u << sh)) | (uint32_t(X) << sh);
+                read4(cbuf, cc, poff, cv);
+                const uint32_t keep = (comp_alive && cy != uint32_t(X)) ? 0xffffffffu : 0u;
+                const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                if (erased_i) {  // S += H_e Out(e, z): Out = gamma * companion (0 where red)
+                    uint32_t v[8];
+#pragma unroll
+                    for (int w = 0; w < 8; w++) v[w] = xor_xtime4_masked(0u, cv[w], ks, kr);
+                    transpose8(v);
+                    fold<I, false>(v, S);
+                }
+                if (used_i) {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
                     transpose8(u);
                     fold<I, false>(u, S);
-                    __builtin_amdgcn_sched_barrier(0);  // one node's values live at a time
-                });
-            } else {
-                // section G as phase_a: per-node uniform branches (used / the one erased node)
-                uint32_t o[4][8];
-                sfor<4>([&](auto xc) BS_INL {
-                    constexpr int X = decltype(xc)::value;
-                    if ((aliveY >> X) & 1u) {
-                        read4(buf_of(X), c, poff, o[X]);
-                    } else {
-#pragma unroll
-                        for (int w = 0; w < 8; w++) o[X][w] = 0;
-                    }
-                });
-                if (xeG >= 0) {  // Out(e_G, slot g) = gamma * C(node (G, g), slot xeG), 0 at slot xeG
-                    uint32_t v[8];
-                    sfor<4>([&](auto gc) BS_INL {
-                        constexpr int g = decltype(gc)::value;
-                        v[2 * g] = v[2 * g + 1] = 0;
-                        sfor<4>([&](auto ac) BS_INL {
-                            constexpr int A = decltype(ac)::value;
-                            if (A != g && xeG == A) {
-                                v[2 * g] = gf_xt(o[g][2 * A]);
-                                v[2 * g + 1] = gf_xt(o[g][2 * A + 1]);
-                            }
-                        });
-                    });
-                    transpose8(v);
-                    sfor<4>([&](auto ac) BS_INL {  // S += H_eG Out(e_G, .)
-                        constexpr int A = decltype(ac)::value;
-                        if (A == xeG) fold<4 * G + A, false>(v, S);
-                    });
                 }
+                if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+            });
+        } else {
+            // section G: all four nodes' slots are in the lane; U(a, g) = C(a, g) + gamma C(g, a)
+            uint32_t o[4][8];
+            sfor<4>([&](auto xc) BS_INL {
+                constexpr int X = decltype(xc)::value;
+                if ((aliveY >> X) & 1u) {
+                    read4(buf_of(X), c, poff, o[X]);
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) o[X][w] = 0;
+                }
+            });
+            if constexpr (RT) {
+                // every erased node (G, A): Out((G, A), slot g) = gamma * C((G, g), slot A), 0 at
+                // slot A and where (G, g) has no data (erased: a both-erased pair, inverted later)
                 sfor<4>([&](auto ac) BS_INL {
                     constexpr int A = decltype(ac)::value;
-                    constexpr int I = 4 * G + A;
-                    if (!((usedY >> A) & 1u)) return;
-                    uint32_t u[8];
-                    sfor<4>([&](auto gc) BS_INL {
-                        constexpr int g = decltype(gc)::value;
-                        const uint32_t keep = (A != g && ((aliveY >> g) & 1u)) ? 0xffffffffu : 0u;
-                        const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
-                        u[2 * g] = xor_xtime4_masked(o[A][2 * g], o[g][2 * A], ks, kr);
-                        u[2 * g + 1] = xor_xtime4_masked(o[A][2 * g + 1], o[g][2 * A + 1], ks, kr);
+                    if (!((emY >> A) & 1u)) return;
+                    uint32_t v[8];
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        v[2 * g] = g == A ? 0u : gf_xt(o[g][2 * A]);
+                        v[2 * g + 1] = g == A ? 0u : gf_xt(o[g][2 * A + 1]);
+                    }
+                    transpose8(v);
+                    fold<4 * G + A, false>(v, S);
+                    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+                });
+            } else if ((CT ? (XE < 4 ? XE : -1) : xeG) >= 0) {
+                // Out(e_G, slot g) = gamma * C(node (G, g), slot xe), 0 at slot xe
+                const int xe = CT ? XE : xeG;
+                uint32_t v[8];
+                sfor<4>([&](auto gc) BS_INL {
+                    constexpr int g = decltype(gc)::value;
+                    v[2 * g] = v[2 * g + 1] = 0;
+                    sfor<4>([&](auto ac) BS_INL {
+                        constexpr int A = decltype(ac)::value;
+                        if (A != g && xe == A) {
+                            v[2 * g] = gf_xt(o[g][2 * A]);
+                            v[2 * g + 1] = gf_xt(o[g][2 * A + 1]);
+                        }
                     });
-                    transpose8(u);
-                    fold<I, false>(u, S);
+                });
+                transpose8(v);
+                sfor<4>([&](auto ac) BS_INL {  // S += H_eG Out(e_G, .)
+                    constexpr int A = decltype(ac)::value;
+                    if (A == xe) fold<4 * G + A, false>(v, S);
                 });
             }
-        });
+            sfor<4>([&](auto ac) BS_INL {
+                constexpr int A = decltype(ac)::value;
+                constexpr int I = 4 * G + A;
+                if (!(CT ? A != XE : ((used_all >> I) & 1u))) return;
+                uint32_t u[8];
+                sfor<4>([&](auto gc) BS_INL {
+                    constexpr int g = decltype(gc)::value;
+                    const uint32_t keep = (A != g && ((aliveY >> g) & 1u)) ? 0xffffffffu : 0u;
+                    const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                    u[2 * g] = xor_xtime4_masked(o[A][2 * g], o[g][2 * A], ks, kr);
+                    u[2 * g + 1] = xor_xtime4_masked(o[A][2 * g + 1], o[g][2 * A + 1], ks, kr);
+                });
+                transpose8(u);
+                fold<I, false>(u, S);
+                if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+        // a distinct marker ends every copy: the copies' common tails are not sunk below phase_a's
+        // switch (that merges S's elements behind pointer phis, which then live in scratch)
+        asm volatile("; phase A copy %0" ::"i"(XE + 1));
     }
 
     // v_perm table i of a table block (8 dwords each, 5 used; decode_args.hpp)

@@ -8,7 +8,8 @@
 // pipeline (measured: memory + phase A 0.51 ms, full 1.05 ms).  Here:
 //   * LDS = a ring of RB = 10 - ne node buffers (16 KiB: one node x 256 layers x 64 B) that
 //     streams continuously across tiles + a separate S/C region (ne x 16 KiB, [row r][z][64 B]);
-//   * 8 compute waves: phase A of tile k (StreamDec::phase_a, one barrier per section), the
+//   * 8 compute waves: phase A of tile k (StreamDec::phase_a, one barrier per section; each
+//     step a copy with the section's erasure structure at compile time, DecArgs::scase), the
 //     presolve S' = H_K^-1 S in registers (check j outer: its row tables through scalar loads
 //     once per tile), then S'(k) into the S/C region (below);
 //   * 4 loader waves issue every LDS-DMA (as in k_stream_syn; the next tile's first loads once
@@ -41,7 +42,7 @@ constexpr int kF2Items = 13;
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
 // 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
 // (workgroup 0 prints the totals of compute wave 0 and loader wave 0), 64 = rounds at priority 0,
-// 128 = phase A with the (10,4,13) {0,4,8,12} masks at compile time
+// 128 = phase A without the per-section compile-time copies (StreamDec::phase_a)
 template <int KD, int G, int PROBE = 0>
 __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(DecArgs a) {
     using Kn = StreamDec<KD, G>;
@@ -254,11 +255,8 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
-            if constexpr ((PROBE & 256) != 0)  // probe: the branch-free phase A
-                Kn::phase_a_bf(a, smem, k * NT, c0, poff0, xeG, S, RB, TM ? &tm_pabar : nullptr);
-            else
-                Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false>(a, smem, k * NT, c0, poff0, xeG, S,
-                                                                                        RB, TM ? &tm_pabar : nullptr);
+            Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false>(a, smem, k * NT, c0, poff0, xeG, S,
+                                                                                    RB, TM ? &tm_pabar : nullptr);
             // bit planes -> bytes
 #pragma unroll
             for (int j = 0; j < 4; j++) {
