@@ -284,6 +284,7 @@ static Tuning read_tuning() {
     t.decode_probe = int(ival("CLAY_DECODE_PROBE", 0));
     const long long ring = ival("CLAY_DECODE_RING", 10);
     t.decode_ring = uint32_t(ring >= 6 && ring <= 10 ? ring : 10);
+    t.local_w64 = ival("CLAY_LOCAL_W64", 0) != 0;
     return t;
 }
 // namespace-scope: initialised when the library is loaded, before any ABI call

@@ -1876,6 +1876,7 @@ static Error dec_tables(CodeState &cs, const DevProps &prop, const std::vector<u
 }
 
 hipError_t launch_stream_local_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
+hipError_t launch_stream_local256_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_local256.hip
 
 // Local decode (stream_local.hpp): erasures in one y-section G (any number) plus at most one
 // erasure in one other section g2 -- every iscore dependency inside a wave, one launch, no
@@ -1914,12 +1915,25 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
     if (g2 >= 0) a.x2 = uint32_t(__builtin_ctz(a.emask[g2]));
     perm_table(gamma_det_inv(), &tabs[bs::kDecDetInv * 8]);  // (1 + gamma^2)^-1, transforms.rs:108-125
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
-    a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
+    // one erasure in section G (plus at most one in g2): the 256-byte-run kernel
+    // (stream_local256.hpp), XCD regions of whole 32-byte units and 256-byte tiles as the encode's
+    const bool w256 = per_sec[G] == 1 && !tuning().local_w64;
+    if (w256) {
+        a.region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
+        a.nslots = std::min(per_xcd, std::max(1u, (a.region + 255u) / 256u));
+    } else {
+        a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
+    }
     e = dec_tables(cs, prop, tabs, stream, &a.tabs);
     if (e) return e;
-    CLAY_HIP(launch_stream_local_kernel(KD, G, a, stream, prop.dev));
+    if (w256) {
+        CLAY_HIP(launch_stream_local256_kernel(KD, G, a, stream, prop.dev));
+        t_last_exec = "stream-local256";
+    } else {
+        CLAY_HIP(launch_stream_local_kernel(KD, G, a, stream, prop.dev));
+        t_last_exec = "stream-local";
+    }
     t_last_launches += 1;
-    t_last_exec = "stream-local";
     *done = true;
     return Error{};
 }

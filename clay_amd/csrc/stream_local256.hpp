@@ -1,0 +1,414 @@
+// stream_local256.hpp -- the local decode on 256-byte row runs, for q = 4, t = 4 codes
+// ((10,4,13), (9,4,12)) with ONE erasure e_G = (G, xg) in a y-section G plus at most one
+// erasure e2 = (g2, x2) in one other section: {0}, {12}, {0,4}, ...  The same algebra as
+// k_stream_local (stream_local.hpp: syndrome form, decode.rs:260-408, iscore order of
+// decode.rs:196-254), on the encode's LDS image (stream_encode.hpp) instead of 64-byte tiles.
+//
+// Why the encode's image fits.  A tile is W = 256 byte positions of every (node, layer) row and is
+// processed as 4 groups b (layer digit G = b) x 4 section steps; step (b, Y) streams the alive
+// nodes of section Y at the 64 layers with digit G = b (one 16 KiB node buffer each: 64 columns c
+// x 256 B, every LDS-DMA instruction 4 whole 256-byte row runs).  Lane = (column c, part p), 32
+// positions ([16p, 16p + 16) and [128 + 16p, +16) of the tile), the same column in every group.
+//   * Sections Y != G couple layers that differ in digit Y only, inside the group: phase A of
+//     k_stream_local (PRT, transpose, RS check fold into the group's syndromes S_b), with the
+//     companion read from the same step's buffers.
+//   * Section G couples group b with the other groups: U((G, X), z) = C((G, X), z) + gamma
+//     C((G, b), z[G := X]).  Its own term folds into S_b; the coupled term is collected by its
+//     SOURCE: node (G, X) streamed at group b != X is the companion of node (G, b) at group X, so
+//     it adds A_(G,b)[r] C((G, X) @ b) to the presolved row r of group X (A_i = H_K^-1 gamma H_i,
+//     the tables the rounds use) -- for (G, b) used, or b = xg (the Out term of e_G).  Nothing of
+//     section G crosses groups in the bit-sliced domain, so a lane carries only S_b (32 registers)
+//     and the presolved rows C_r(group) (8 registers per erased row and group).
+//   * End of group b: C_r(b) += row e_r of H_K^-1 S_b (the presolve, byte domain).
+//   * After the four groups, the solve of k_stream_local with "slot" = group: (i) g2-lines of the
+//     groups != xg (lanes l ^ 8, l ^ 16: section g2's digit is at bits 0-1 of c), (ii) group xg:
+//     the dropped terms A_(G,A) C_eG(group A) of the used (G, A), in-lane, (iii) g2-lines of group
+//     xg.  Each step reads only values the previous steps finished.
+// The loader waves, the ring (a.ring - 1 node buffers streaming continuously across groups and
+// tiles; the tables in the last buffer) and the counted waits follow k_stream_local; the tile map
+// and the partial-tile handling (the piece straddling the end of an sc % 16 == 8 row rewritten
+// in LDS after landing) follow k_stream_encode.
+#pragma once
+
+#include "stream_decode.hpp"
+
+namespace clay {
+namespace bs {
+
+template <int KD, int G, int NE>
+struct Local256 {
+    using D = StreamDec<KD, G>;
+    static_assert(NE == 1 || NE == 2, "one erasure in section G plus at most one more");
+    static constexpr int W = 256, CWAVES = 8, LOADERS = 4, BLOCK = 64 * (CWAVES + LOADERS);
+    static constexpr int BUF = 16384;  // 64 columns x 256 B
+    static constexpr int BPL = 16 / LOADERS;
+    static constexpr int LDS_BYTES = 10 * BUF;
+
+    // node-buffer image of the encode (stream_encode.hpp sw()): row c at [256 c, 256 c + 256),
+    // its 16-byte piece k at slot k ^ sw(c)
+    __host__ __device__ static constexpr uint32_t sw(uint32_t c) { return ((c >> 1) & 1u) * 8u; }
+    __device__ static uint32_t piece0(uint32_t c, uint32_t p) { return c * 256u + ((p ^ sw(c)) << 4); }
+    // the lane's 32 bytes (pieces p and 8 + p) of a node buffer
+    __device__ static void read32(const uint8_t *buf, uint32_t o0, uint32_t (&d)[8]) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(buf + o0);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(buf + (o0 ^ 128u));
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = v0.w;
+        d[4] = v1.x; d[5] = v1.y; d[6] = v1.z; d[7] = v1.w;
+    }
+
+    // ---------------- loader ----------------
+    struct Loader {
+        uint32_t off[BPL];  // layer0(column) * sc + 16 * piece, per block
+        uint32_t k16, rl;
+        int li;
+    };
+    __device__ static void loader_init(Loader &L, const DecArgs &a, int li, int lane) {
+        const uint32_t sc = uint32_t(a.sc);
+        L.li = li;
+        L.rl = uint32_t(lane) >> 4;
+        L.k16 = ((uint32_t(lane) & 15u) ^ sw(L.rl)) * 16u;
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            const uint32_t c = uint32_t(li * BPL + j) * 4u + L.rl;
+            L.off[j] = D::layer0_rt(a, c) * sc + L.k16;
+        }
+    }
+    // node buffer at LDS address lds_buf <- 64 layers (digit G = b) x the tile of node
+    __device__ static void issue(const DecArgs &a, const Loader &L, uint32_t lds_buf, const uint8_t *node, StreamTile t,
+                                 uint32_t b) {
+        const uint32_t sc = uint32_t(a.sc);
+        lds_buf = __builtin_amdgcn_readfirstlane(lds_buf) + uint32_t(L.li * BPL) * 1024u;
+        const uint64_t gofs = uint64_t(b * D::wt(G)) * sc;
+        if (t.vend >= t.b0 + uint32_t(W)) {
+            const uint8_t *base = uniform_ptr(node + gofs + t.b0);
+#pragma unroll
+            for (int j = 0; j < BPL; j++) dma16(lds_buf + uint32_t(j) * 1024u, base, L.off[j]);
+        } else {
+            // partial tile: a piece straddling vend is read from vend - 16 (patched after
+            // landing), a piece wholly past vend from there too (never used)
+            const uint8_t *base = uniform_ptr(node + gofs);
+            uint32_t pos = t.b0 + L.k16;
+            if (pos + 16u > t.vend) pos = t.vend - 16u;  // vend >= 16 (sc >= 512)
+#pragma unroll
+            for (int j = 0; j < BPL; j++) dma16(lds_buf + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
+        }
+    }
+    // sc % 16 == 8 tile end: the straddling piece of every row holds 8 valid bytes; rewrite it
+    // in LDS from global memory once the step's DMA has landed
+    __device__ static void patch(const DecArgs &a, const Loader &L, uint8_t *buf, const uint8_t *node, StreamTile t,
+                                 uint32_t b, int lane) {
+        const uint32_t sc = uint32_t(a.sc), pos = t.b0 + L.k16;
+        if (!(pos < t.vend && pos + 16u > t.vend)) return;
+#pragma unroll
+        for (int j = 0; j < BPL; j++) {
+            const int blk = L.li * BPL + j;
+            const uint64_t o = uint64_t(L.off[j] - L.k16) + uint64_t(b * D::wt(G)) * sc + pos;
+            const uint2 gv = *reinterpret_cast<const uint2 *>(node + o);
+            *reinterpret_cast<uint4 *>(buf + blk * 1024 + lane * 16) = make_uint4(gv.x, gv.y, 0u, 0u);
+        }
+    }
+
+    // ---------------- compute helpers ----------------
+    // C_r rows of the lane: R_[r][group][8 dwords] (byte domain)
+    using Rows = uint32_t[NE][4][8];
+    // row r (uniform at run time) of group gi: opaque masks, not selects (a select between
+    // register arrays becomes a dynamic index and moves them to scratch)
+    __device__ static void get(const Rows &C, uint32_t r, int gi, uint32_t (&v)[8]) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) v[w] = 0;
+#pragma unroll
+        for (int k = 0; k < NE; k++) {
+            const uint32_t m = opq(r == uint32_t(k) ? 0xffffffffu : 0u);
+#pragma unroll
+            for (int w = 0; w < 8; w++) v[w] |= C[k][gi][w] & m;
+        }
+    }
+    // C_r(group gi) ^= T_r * v for every erased row r
+    __device__ static void add_mul(Rows &C, const uint8_t *tl, int tab0, const uint32_t (&v)[8], int gi) {
+        GfTab tb[NE];
+#pragma unroll
+        for (int r = 0; r < NE; r++) tb[r] = D::tab_at(tl, tab0 + r);
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            const GfIdx ix = gf_idx(v[w]);
+#pragma unroll
+            for (int r = 0; r < NE; r++) C[r][gi][w] ^= gf_mul_idx(ix, tb[r]);
+        }
+    }
+    // steps (i) / (iii): group gi, terms of the g2-line (lanes differing in bits 3-4)
+    __device__ static void line_g2(const DecArgs &a, Rows &C, const uint8_t *tl, uint32_t c, int gi) {
+        const uint32_t g2 = uint32_t(a.g2), x2 = a.x2;
+        const uint32_t d2 = c & 3u;  // this lane's digit of section g2
+        const uint32_t r2 = uint32_t(a.rix[4 * g2 + x2]);
+        const bool red = d2 == x2;
+        const bool src = !red && ((a.used >> (4u * g2 + d2)) & 1u);
+        const int ti = int(16u + (4u * g2 + d2) * 4u);  // per-lane table row (d2 varies over the line)
+        uint32_t v[8];
+        get(C, r2, gi, v);
+        GfTab tb[NE];
+#pragma unroll
+        for (int r = 0; r < NE; r++) tb[r] = D::tab_at(tl, ti + r);
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            const GfIdx ix = gf_idx(src ? v[w] : 0u);
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
+                uint32_t t = gf_mul_idx(ix, tb[r]);
+                t ^= uint32_t(__shfl_xor(int(t), 8));
+                t ^= uint32_t(__shfl_xor(int(t), 16));
+                if (red) C[r][gi][w] ^= t;
+            }
+        }
+    }
+
+    // one step (group b, section Y): S_b += the section's terms; section G's coupled terms into C
+    template <int Y>
+    __device__ __forceinline__ static void step(const DecArgs &a, uint8_t *smem, uint32_t gbase, uint32_t R, uint32_t c,
+                                                uint32_t p, uint32_t b, uint32_t xg, uint32_t (&S)[32], Rows &C,
+                                                const uint8_t *tl) {
+        uint32_t alive_all = __builtin_amdgcn_readfirstlane(a.alive), used_all = __builtin_amdgcn_readfirstlane(a.used),
+                 emY = __builtin_amdgcn_readfirstlane(a.emask[Y]);
+        asm volatile("" : "+s"(alive_all), "+s"(used_all), "+s"(emY));
+        const uint32_t aliveY = (alive_all >> (4 * Y)) & 15u;
+        const uint32_t rs = a.sec_off[Y];
+        auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
+            const uint32_t q = rs + uint32_t(__builtin_popcount(aliveY & ((1u << x) - 1u)));
+            return smem + ((gbase + q) % R) * BUF;
+        };
+        const uint32_t own0 = piece0(c, p);
+        if constexpr (Y != G) {
+            const uint32_t sh = a.csh[Y];
+            const uint32_t cy = (c >> sh) & 3u;
+            const bool comp_alive = (aliveY >> cy) & 1u;
+            const uint8_t *cbuf = comp_alive ? buf_of(cy) : smem;
+            sfor<4>([&](auto xc) BS_INL {
+                constexpr int X = decltype(xc)::value;
+                constexpr int I = 4 * Y + X;
+                const bool alive_i = (aliveY >> X) & 1u;
+                const bool used_i = (used_all >> I) & 1u;
+                const bool erased_i = (emY >> X) & 1u;
+                if (!(used_i || erased_i)) return;
+                uint32_t o[8], cv[8], u[8];
+                if (alive_i) {
+                    read32(buf_of(X), own0, o);
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) o[w] = 0;
+                }
+                const uint32_t cc = (c & ~(3u << sh)) | (uint32_t(X) << sh);
+                read32(cbuf, piece0(cc, p), cv);
+                const uint32_t keep = (comp_alive && cy != uint32_t(X)) ? 0xffffffffu : 0u;
+                const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+                if (erased_i) {  // S += H_e Out(e, z): Out = gamma * companion (0 where red)
+                    uint32_t v[8];
+#pragma unroll
+                    for (int w = 0; w < 8; w++) v[w] = xor_xtime4_masked(0u, cv[w], ks, kr);
+                    transpose8(v);
+                    D::template fold<I, false>(v, S);
+                }
+                if (used_i) {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) u[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+                    transpose8(u);
+                    D::template fold<I, false>(u, S);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        } else {
+            // the coupled terms of group b's sources go to group X: coefficient A_(G,b)[r] when
+            // (G, b) is used, or is e_G (its Out term); none from the red node (G, b) itself
+            const bool cross = ((used_all >> (4 * G + b)) & 1u) || b == xg;
+            sfor<4>([&](auto xc) BS_INL {
+                constexpr int X = decltype(xc)::value;
+                constexpr int I = 4 * G + X;
+                if (!((aliveY >> X) & 1u)) return;
+                uint32_t o[8];
+                read32(buf_of(X), own0, o);
+                if (cross && uint32_t(X) != b) add_mul(C, tl, int(16u + (4u * G + b) * 4u), o, X);
+                if ((used_all >> I) & 1u) {
+                    transpose8(o);
+                    D::template fold<I, false>(o, S);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+    }
+};
+
+// grid = 8 * nslots (one workgroup per CU); LDS = 10 x 16 KiB: a ring of a.ring - 1 node
+// buffers and the tables (presolve, A_i) in the last.  a.region: XCD region bytes (multiple of 32).
+template <int KD, int G, int NE>
+__global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local256(DecArgs a) {
+    using Kn = Local256<KD, G, NE>;
+    using D = typename Kn::D;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7u, wslot = blockIdx.x >> 3, ns = a.nslots;
+    const uint32_t sc = uint32_t(a.sc);
+    const StreamMap tm(sc, a.region, ns, xcd, wslot);
+    const uint32_t ntile = uint32_t(tm.ntile());
+    if (ntile == 0) return;  // uniform per workgroup
+    const uint32_t R = a.ring - 1u, NT = a.nt;
+    constexpr uint32_t BUF = uint32_t(Kn::BUF);
+
+    if (wave >= Kn::CWAVES) {
+        // ---------------- loader waves: load l -> buffer l % R, 4 groups x NT loads per tile ----------------
+        __builtin_amdgcn_s_setprio(3);
+        typename Kn::Loader L;
+        Kn::loader_init(L, a, wave - Kn::CWAVES, lane);
+        const uint32_t lds0 = lds_addr_of(smem);
+        if (L.li < 3)  // tables, before any ring load: the first step's counted wait covers them
+            dma16(lds0 + R * BUF + uint32_t(L.li) * 1024u, uniform_ptr(reinterpret_cast<const uint8_t *>(a.tabs)),
+                  uint32_t(L.li) * 1024u + uint32_t(lane) * 16u);
+        const uint32_t NG = 4u * NT;  // loads per tile
+        const uint32_t nloads = ntile * NG;
+        uint32_t issued = 0;
+        auto issue_upto = [&](uint32_t lim) {
+            if (lim > nloads) lim = nloads;
+            for (; issued < lim; issued++) {
+                const uint32_t k = issued / NG, rem = issued % NG, b = rem / NT, q = rem % NT;
+                Kn::issue(a, L, lds0 + (issued % R) * BUF, a.node[a.load_node[q]], tm.tile(int(k), wslot, ns), b);
+            }
+        };
+        issue_upto(R);
+        for (uint32_t k = 0; k < ntile; k++) {
+            const StreamTile t = tm.tile(int(k), wslot, ns);
+            const bool straddle = t.vend < t.b0 + uint32_t(Kn::W) && ((t.vend - t.b0) & 15u);
+            for (uint32_t b = 0; b < 4; b++) {
+                const uint32_t gb = (k * 4u + b) * NT;
+                for (int y = 0; y < 4; y++) {
+                    const uint32_t q0 = gb + a.sec_off[y], qend = gb + a.sec_off[y + 1];
+                    if (straddle) {
+                        wait_vm0();
+                        for (uint32_t l = q0; l < qend; l++)
+                            Kn::patch(a, L, smem + (l % R) * BUF, a.node[a.load_node[l % NT]], t, b, lane);
+                    } else {
+                        wait_vm_rt(int((issued - qend) * uint32_t(Kn::BPL)));
+                    }
+                    lds_barrier();
+                    issue_upto(q0 + R);
+                }
+            }
+        }
+        wait_vm0();
+        return;
+    }
+
+    // ---------------- compute waves ----------------
+    const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p0 = uint32_t(threadIdx.x) & 7u;
+    const uint32_t eG = a.emask[G];
+    const uint32_t xg = uint32_t(__builtin_ctz(eG));
+    const bool has2 = a.g2 >= 0;
+    for (uint32_t k = 0; k < ntile; k++) {
+        const StreamTile t = tm.tile(int(k), wslot, ns);
+        uint32_t C[NE][4][8];
+#pragma unroll
+        for (int r = 0; r < NE; r++)
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+#pragma unroll
+                for (int w = 0; w < 8; w++) C[r][g][w] = 0;
+#pragma unroll 1
+        for (uint32_t b = 0; b < 4; b++) {
+            uint32_t S[32];
+#pragma unroll
+            for (int w = 0; w < 32; w++) S[w] = 0;
+            const uint32_t gb = (k * 4u + b) * a.nt;
+            sfor<4>([&](auto yc) BS_INL {
+                constexpr int Y = decltype(yc)::value;
+                lds_barrier();  // step (k, b, Y) landed
+                const uint8_t *tl = smem + R * BUF + opq(0u);
+                Kn::template step<Y>(a, smem, gb, R, opq(c0), opq(p0), b, xg, S, C, tl);
+            });
+            // end of group b: C_r(b) += row e_r of H_K^-1 S_b (bit planes -> bytes, then v_perm)
+            const uint8_t *tl = smem + R * BUF + opq(0u);
+            uint32_t T[NE][8];
+#pragma unroll
+            for (int r = 0; r < NE; r++)
+#pragma unroll
+                for (int w = 0; w < 8; w++) T[r][w] = 0;
+            sfor<4>([&](auto jc) BS_INL {
+                constexpr int j = decltype(jc)::value;
+                uint32_t v[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++) v[w] = S[j * 8 + w];
+                transpose8(v);
+                GfTab tb[NE];
+#pragma unroll
+                for (int r = 0; r < NE; r++) tb[r] = D::tab_at(tl, r * 4 + j);
+#pragma unroll
+                for (int w = 0; w < 8; w++) {
+                    const GfIdx ix = gf_idx(v[w]);
+#pragma unroll
+                    for (int r = 0; r < NE; r++) T[r][w] ^= gf_mul_idx(ix, tb[r]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            sfor<4>([&](auto gc) BS_INL {
+                constexpr int g = decltype(gc)::value;
+                if (b != uint32_t(g)) return;
+#pragma unroll
+                for (int r = 0; r < NE; r++)
+#pragma unroll
+                    for (int w = 0; w < 8; w++) C[r][g][w] ^= T[r][w];
+            });
+        }
+        const uint8_t *tl = smem + R * BUF + opq(0u);
+        const uint32_t c = opq(c0), p = opq(p0);
+        // (i) g2-lines of the groups != xg (sources: level-0 values)
+        if (has2) {
+            sfor<4>([&](auto gc) BS_INL {
+                constexpr int g = decltype(gc)::value;
+                if (uint32_t(g) != xg) Kn::line_g2(a, C, tl, c, g);
+            });
+        }
+        // (ii) group xg: the in-lane terms of the used nodes (G, A), A != xg
+        {
+            const uint32_t rg = uint32_t(a.rix[4 * G + xg]);
+            const uint32_t used_all = a.used;
+            sfor<4>([&](auto gc) BS_INL {
+                constexpr int g = decltype(gc)::value;
+                if (uint32_t(g) != xg) return;
+                sfor<4>([&](auto ac) BS_INL {
+                    constexpr int A = decltype(ac)::value;
+                    if (A == g || !((used_all >> (4 * G + A)) & 1u)) return;
+                    uint32_t v[8];
+                    Kn::get(C, rg, A, v);
+                    Kn::add_mul(C, tl, 16 + (4 * G + A) * 4, v, g);
+                });
+            });
+        }
+        // (iii) red lanes of the g2-lines of group xg (sources final after (ii))
+        if (has2) {
+            sfor<4>([&](auto gc) BS_INL {
+                constexpr int g = decltype(gc)::value;
+                if (uint32_t(g) == xg) Kn::line_g2(a, C, tl, c, g);
+            });
+        }
+        // outputs: pieces p and 8 + p of row (layer z) per erased row and group
+        const uint32_t z0 = D::layer0_rt(a, c);
+        const bool full = t.vend >= t.b0 + uint32_t(Kn::W);
+#pragma unroll
+        for (int r = 0; r < NE; r++) {
+            uint8_t *dst = a.out[r];
+            if (!dst) continue;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                uint8_t *row = dst + uint64_t(z0 + uint32_t(g) * D::wt(G)) * sc + t.b0 + 16u * p;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t pos = t.b0 + 16u * p + 128u * uint32_t(h);
+                    const uint32_t nv = full ? 16u : (pos >= t.vend ? 0u : (t.vend - pos >= 16u ? 16u : t.vend - pos));
+                    if (nv == 16u)
+                        *reinterpret_cast<uint4 *>(row + 128 * h) =
+                            make_uint4(C[r][g][4 * h], C[r][g][4 * h + 1], C[r][g][4 * h + 2], C[r][g][4 * h + 3]);
+                    else if (nv >= 8u)
+                        *reinterpret_cast<uint2 *>(row + 128 * h) = make_uint2(C[r][g][4 * h], C[r][g][4 * h + 1]);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace bs
+}  // namespace clay

@@ -36,6 +36,8 @@ struct Tuning {
     // streaming decodes: LDS node buffers of the ring (6..10; the split syn kernel and the local
     // kernel use one less, the last holds the tables)
     uint32_t decode_ring = 10;   // CLAY_DECODE_RING
+    // local decode: the 64-byte-tile kernel also for one erasure in section G (A/B measurements)
+    bool local_w64 = false;      // CLAY_LOCAL_W64
 };
 
 // The knobs as read at load time.

@@ -169,6 +169,11 @@ if __name__ == "__main__":
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4])),
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 2, 3])),
             ("decodeL", lambda: decode_cfg(10, 4, 13, 1 << 30, [12])),
+            # the local decodes: 256-byte row runs ({0}, {12}, {0,4}) and 64-byte tiles ({0,1})
+            ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [0])),
+            ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [12])),
+            ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
+            ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1])),
             # clay_decode_device_codeword: one erasure rebuilt by the repair kernel from whole
             # chunks (charged the repair route's bytes)
             ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [0], codeword=True)),

@@ -149,6 +149,52 @@ def _syndromes_presolved(code, C, E, used, rows):
     return V
 
 
+def presolved_by_source(code, C, E, used, rows, A, G):
+    """k_stream_local256's phase A (stream_local256.hpp) for one erased node in section G: per
+    group b (digit G = b) S_b takes the sections != G as above and only the OWN terms H_i C(i, z)
+    of section G; the coupled terms gamma H_(G,b) C((G, X), z[G := b]) of section G are collected
+    by source -- node (G, X) at group b != X adds A_(G,b)[r] C((G, X), z') to row r at z'[G := X]
+    when (G, b) is used or erased (its Out term).  Equals _syndromes_presolved."""
+    Eset = set(E)
+    sc = C.shape[2]
+    V = np.zeros((len(E), 256, sc), dtype=np.uint8)
+    for z in range(256):
+        S = np.zeros((4, sc), dtype=np.uint8)
+        for i in range(16):
+            y, x = divmod(i, 4)
+            zy = code.digit(z, y)
+            comp = 4 * y + zy
+            zs = code.with_digit(z, y, x)
+            if y == G:
+                if i in used:
+                    u = C[i, z]
+                else:
+                    continue
+            elif i in used:
+                u = C[i, z].copy()
+                if zy != x and comp not in Eset:
+                    u ^= gmul(GAMMA, C[comp, zs])
+            elif i in Eset and zy != x and comp not in Eset:
+                u = gmul(GAMMA, C[comp, zs])
+            else:
+                continue
+            for p in range(4):
+                S[p] ^= gmul(code.H[p, i], u)
+        for r in range(len(E)):
+            for j in range(4):
+                V[r, z] ^= gmul(rows[r][j], S[j])
+        b = code.digit(z, G)
+        if (4 * G + b) in used or (4 * G + b) in Eset:
+            for X in range(4):
+                src = 4 * G + X
+                if X == b or src in Eset:
+                    continue  # the red node; an erased source has no data (dropped, solve step ii)
+                zt = code.with_digit(z, G, X)
+                for r in range(len(E)):
+                    V[r, zt] ^= gmul(A[4 * G + b][r], C[src, z])
+    return V
+
+
 def local_eligible(code, erased_ext):
     per = [0] * 4
     for e in erased_ext:

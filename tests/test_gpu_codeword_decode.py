@@ -58,7 +58,7 @@ def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda):
         ref = o.encode_array(np.random.default_rng(sc + len(er)).integers(0, 256, c.k * chunk, dtype=np.uint8))
         full = torch.from_numpy(ref).cuda()
         outs = _decode_dev(torch, c, full, er, chunk)
-        assert clay_amd.last_exec_path() == "stream-local", (sc, er, clay_amd.last_exec_path())
+        assert clay_amd.last_exec_path() == "stream-local256", (sc, er, clay_amd.last_exec_path())
         for e in er:
             assert np.array_equal(outs[e].numpy(), ref[e]), (sc, er, e)
 
@@ -72,7 +72,7 @@ def test_plain_decode_keeps_decode_semantics_on_non_codewords(oracle_mod, torch_
     chunk = c.sub_chunk_no * sc
     chunks = np.random.default_rng(3).integers(0, 256, (c.n, chunk), dtype=np.uint8)
     outs = _decode_dev(torch, c, torch.from_numpy(chunks).cuda(), [2], chunk, codeword=False)
-    assert clay_amd.last_exec_path() == "stream-local"
+    assert clay_amd.last_exec_path() == "stream-local256"
     av = {i: chunks[i] for i in range(c.n) if i != 2}
     ref = np.frombuffer(o.decode(av, [2]), dtype=np.uint8).reshape(c.k, -1)
     assert np.array_equal(outs[2].numpy(), ref[2])
@@ -118,4 +118,4 @@ def test_codeword_call_does_not_change_concurrent_decodes(oracle_mod, torch_cuda
     for t in ts:
         t.join()
     assert not errors, errors
-    assert paths == {"a": {"bs-repair-stream"}, "b": {"stream-local"}}, paths
+    assert paths == {"a": {"bs-repair-stream"}, "b": {"stream-local256"}}, paths

@@ -50,7 +50,10 @@ def local_eligible(c, er):
 def stream_path(c, er):
     """The kernel exec mode "stream" runs a pattern on (None: the plan executor)."""
     if local_eligible(c, er):
-        return "stream-local"
+        per = [0] * c.t
+        for e in er:
+            per[_internal(c, e) // c.q] += 1
+        return "stream-local256" if max(per) == 1 else "stream-local"
     if fused2_eligible(c, er):
         return "stream-fused2"
     return None

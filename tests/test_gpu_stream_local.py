@@ -1,5 +1,6 @@
-"""GPU parity of the local streaming decode (stream_local.hpp, exec mode "stream-local" and auto)
-against the oracle.
+"""GPU parity of the local streaming decodes (exec mode "stream-local" and auto) against the
+oracle: k_stream_local256 (stream_local256.hpp, 256-byte row runs) for one erasure in a section
+plus at most one in another, k_stream_local (stream_local.hpp, 64-byte tiles) for the rest.
 
 The kernel serves q = 4, t = 4 codes ((10,4,13), (9,4,12)) whose erasures lie in one y-section
 plus at most one erasure in one other section: single erasures, two erasures in two sections
@@ -28,6 +29,14 @@ def local_eligible(c, er):
         per[_internal(c, e) // c.q] += 1
     nz = sorted([p for p in per if p], reverse=True)
     return 1 <= len(er) <= c.m and len(nz) <= 2 and (len(nz) < 2 or nz[1] == 1)
+
+
+def local_path(c, er):
+    """The local kernel a local-eligible pattern runs on."""
+    per = [0] * c.t
+    for e in er:
+        per[_internal(c, e) // c.q] += 1
+    return "stream-local256" if max(per) == 1 else "stream-local"
 
 
 def _local_patterns(c, seed, n3, n4):
@@ -72,7 +81,7 @@ def test_local_decode_random_inputs(oracle_mod, torch_cuda, local_mode, cfg, sc)
         got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
         path = clay_amd.last_exec_path()
         if local_eligible(c, er):
-            assert path == "stream-local", (er, path)
+            assert path == local_path(c, er), (er, path)
             n_local += 1
         av = {i: chunks[i] for i in range(c.n) if i not in er}
         ref = np.frombuffer(o.decode(av, er), dtype=np.uint8).reshape(c.k, -1)
@@ -98,7 +107,7 @@ def test_local_decode_codeword_incl_parity(oracle_mod, torch_cuda, local_mode, c
     for er in pats:
         assert local_eligible(c, er), er
         got = _decode_dev(torch, c, ref, er, chunk)
-        assert clay_amd.last_exec_path() == "stream-local", er
+        assert clay_amd.last_exec_path() == local_path(c, er), er
         for e in er:
             assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e)
 
@@ -116,7 +125,7 @@ def test_local_decode_matches_grouped_incl_parity(oracle_mod, torch_cuda, er):
     prev = clay_amd.set_exec_mode("stream-local")
     try:
         a = _decode_dev(torch, c, chunks, er, chunk)
-        assert clay_amd.last_exec_path() == "stream-local"
+        assert clay_amd.last_exec_path() == local_path(c, er)
         clay_amd.set_exec_mode("grouped")
         b = _decode_dev(torch, c, chunks, er, chunk)
         assert clay_amd.last_exec_path() == "grouped"

@@ -61,3 +61,28 @@ def test_fused_rounds_algebra_matches_oracle(oracle_mod, k):
     pats.insert(0, [0, 4, 8, 12] if k == 10 else [0, 4, 8, 11])
     for i, er in enumerate(pats[:20]):
         _check(oracle_mod, code, o, emu.fused_decode, er, 2, 300 * k + i)
+
+
+@pytest.mark.parametrize("k", [10, 9])
+def test_local256_phase_a_by_source_matches(oracle_mod, k):
+    """k_stream_local256's section-G terms collected by source give the same presolved rows as
+    the per-layer phase A, for every pattern with one erasure in its section plus at most one."""
+    code = emu.Code(oracle_mod, k)
+    rng = np.random.default_rng(k)
+    sc = 3
+    pats = [[e] for e in range(code.n)] + [list(p) for p in itertools.combinations(range(code.n), 2)]
+    n = 0
+    for er in pats:
+        per = [0] * 4
+        for e in er:
+            per[code.internal(e) // 4] += 1
+        if max(per) != 1:
+            continue
+        chunks = rng.integers(0, 256, (code.n, 256 * sc), dtype=np.uint8)
+        C, E, used, rows, A = emu._setup(code, chunks, er)
+        G = code.internal(er[0]) // 4
+        want = emu._syndromes_presolved(code, C, E, used, rows)
+        got = emu.presolved_by_source(code, C, E, used, rows, A, G)
+        assert np.array_equal(got, want), er
+        n += 1
+    assert n > 50
