@@ -386,24 +386,51 @@ __global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local25
             });
         }
         // outputs: pieces p and 8 + p of row (layer z) per erased row and group
-        const uint32_t z0 = D::layer0_rt(a, c);
         const bool full = t.vend >= t.b0 + uint32_t(Kn::W);
+        if (full) {
+            // lanes c and c ^ 1 (lane ^ 8) swap halves by DPP (as the encode's parity stores), so
+            // each 16-byte store instruction of a wave writes 4 whole 256-byte row runs
+            const bool odd = c & 1u;
+            const uint32_t ze = D::layer0_rt(a, c & ~1u), zo = D::layer0_rt(a, c | 1u);
+            const uint32_t prel = t.b0 + 16u * p + (odd ? 128u : 0u);
 #pragma unroll
-        for (int r = 0; r < NE; r++) {
-            uint8_t *dst = a.out[r];
-            if (!dst) continue;
+            for (int r = 0; r < NE; r++) {
+                const uint8_t *base = uniform_ptr(a.out[r]);
+                if (!base) continue;
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                uint8_t *row = dst + uint64_t(z0 + uint32_t(g) * D::wt(G)) * sc + t.b0 + 16u * p;
+                for (int g = 0; g < 4; g++) {
+                    uint32_t lo[4], hi[4];
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint32_t pos = t.b0 + 16u * p + 128u * uint32_t(h);
-                    const uint32_t nv = full ? 16u : (pos >= t.vend ? 0u : (t.vend - pos >= 16u ? 16u : t.vend - pos));
-                    if (nv == 16u)
-                        *reinterpret_cast<uint4 *>(row + 128 * h) =
-                            make_uint4(C[r][g][4 * h], C[r][g][4 * h + 1], C[r][g][4 * h + 2], C[r][g][4 * h + 3]);
-                    else if (nv >= 8u)
-                        *reinterpret_cast<uint2 *>(row + 128 * h) = make_uint2(C[r][g][4 * h], C[r][g][4 * h + 1]);
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t send = odd ? C[r][g][i] : C[r][g][4 + i];
+                        const uint32_t rv = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, false));  // row_ror:8
+                        lo[i] = odd ? rv : C[r][g][i];      // row of the even column
+                        hi[i] = odd ? C[r][g][4 + i] : rv;  // row of the odd column
+                    }
+                    const uint32_t zg = uint32_t(g) * D::wt(G);
+                    st16sp<0>(base, (ze + zg) * sc + prel, lo[0], lo[1], lo[2], lo[3]);
+                    st16sp<0>(base, (zo + zg) * sc + prel, hi[0], hi[1], hi[2], hi[3]);
+                }
+            }
+        } else {
+            const uint32_t z0 = D::layer0_rt(a, c);
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
+                uint8_t *dst = a.out[r];
+                if (!dst) continue;
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    uint8_t *row = dst + uint64_t(z0 + uint32_t(g) * D::wt(G)) * sc + t.b0 + 16u * p;
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t pos = t.b0 + 16u * p + 128u * uint32_t(h);
+                        const uint32_t nv = pos >= t.vend ? 0u : (t.vend - pos >= 16u ? 16u : t.vend - pos);
+                        if (nv == 16u)
+                            *reinterpret_cast<uint4 *>(row + 128 * h) =
+                                make_uint4(C[r][g][4 * h], C[r][g][4 * h + 1], C[r][g][4 * h + 2], C[r][g][4 * h + 3]);
+                        else if (nv >= 8u)
+                            *reinterpret_cast<uint2 *>(row + 128 * h) = make_uint2(C[r][g][4 * h], C[r][g][4 * h + 1]);
+                    }
                 }
             }
         }
