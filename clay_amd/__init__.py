@@ -129,7 +129,7 @@ def set_exec_mode(mode: str) -> str:
 
 def last_exec_path() -> str:
     """Plan executor of this thread's last decode / repair / staged encode: 'tile' | 'grouped' |
-    'stream-local' | 'stream-fused2' | 'bs-repair-stream' | 'bs-repair' | 'none'."""
+    'stream-local256' | 'stream-local' | 'stream-fused2' | 'bs-repair-stream' | 'bs-repair' | 'none'."""
     return _lib.lib().clay_last_exec_path().decode()
 
 

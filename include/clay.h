@@ -287,7 +287,9 @@ int clay_set_encode_path(int mode);
  *                per-level executor; for q = 4, t = 4 codes ((10,4,13), (9,4,12)) with
  *                sc % 8 == 0, sc >= 512: decodes whose erasures lie in one y-section plus at
  *                most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4}, {0,1,2,3},
- *                ...) run the single-launch local decode (k_stream_local, last path
+ *                ...) run a single-launch local decode: one erasure in its section plus
+ *                at most one more ({0}, {12}, {0,4}) on 256-byte row runs (k_stream_local256,
+ *                last path "stream-local256"), the others on 64-byte tiles (k_stream_local,
  *                "stream-local"); 3 or 4 erasures in distinct y-sections (the BASELINE
  *                {0,4,8,12} included) the fused decode v2 (k_stream_fused2, "stream-fused2")
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
@@ -299,18 +301,21 @@ int clay_set_encode_path(int mode);
  *   3 stream  -- every decode a streaming kernel takes on it: the local decode where it takes
  *                the pattern, else the fused decode v2 (2-4 erasures in distinct sections);
  *                everything else as auto
- *   5 stream-local -- every decode the local kernel takes on it ("stream-local"); else as auto
+ *   5 stream-local -- every decode a local kernel takes on it ("stream-local256" /
+ *                "stream-local"); else as auto
  *   6 stream-fused2 -- decodes of 2-4 erasures in distinct y-sections on the fused decode v2
  *                (k_stream_fused2, "stream-fused2"; ring of 10 - e node buffers: any two
  *                neighbouring sections hold <= 10 - e surviving real nodes); else as auto
  * (4 and 7 are retired: the single-launch decode of round 3 and the process-wide "codeword"
  * mode, now the per-call clay_decode_device_codeword.)
- * No CLAY_* environment variable changes which kernel a call runs; the measurement knobs
- * (planner and executor tuning) are read once when the library is loaded.
+ * No CLAY_* environment variable is read on a call path; the measurement knobs (planner and
+ * executor tuning, CLAY_LOCAL_W64 = the 64-byte local kernel for every local pattern) are read
+ * once when the library is loaded.
  * Returns the previous mode, or -1 for an unknown mode (setting unchanged). */
 int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
- * "tile" (k_texec), "grouped" (k_gexec), "stream-local" (k_stream_local), "stream-fused2"
+ * "tile" (k_texec), "grouped" (k_gexec), "stream-local256" (k_stream_local256), "stream-local"
+ * (k_stream_local), "stream-fused2"
  * (k_stream_fused2), "bs-repair-stream" (k_bs_repair_stream), "bs-repair" (k_bs_repair) or
  * "none". */
 const char *clay_last_exec_path(void);
