@@ -1915,9 +1915,10 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
     if (g2 >= 0) a.x2 = uint32_t(__builtin_ctz(a.emask[g2]));
     perm_table(gamma_det_inv(), &tabs[bs::kDecDetInv * 8]);  // (1 + gamma^2)^-1, transforms.rs:108-125
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
-    // one erasure in section G (plus at most one in g2): the 256-byte-run kernel
-    // (stream_local256.hpp), XCD regions of whole 32-byte units and 256-byte tiles as the encode's
-    const bool w256 = per_sec[G] == 1 && !tuning().local_w64;
+    // one erasure in section G plus at most one in g2, or two in G and none elsewhere: the
+    // 256-byte-run kernel (stream_local256.hpp), XCD regions of whole 32-byte units and 256-byte
+    // tiles as the encode's
+    const bool w256 = (per_sec[G] == 1 || (per_sec[G] == 2 && g2 < 0)) && !tuning().local_w64;
     if (w256) {
         a.region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
         a.nslots = std::min(per_xcd, std::max(1u, (a.region + 255u) / 256u));

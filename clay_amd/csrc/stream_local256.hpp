@@ -1,6 +1,7 @@
 // stream_local256.hpp -- the local decode on 256-byte row runs, for q = 4, t = 4 codes
-// ((10,4,13), (9,4,12)) with ONE erasure e_G = (G, xg) in a y-section G plus at most one
-// erasure e2 = (g2, x2) in one other section: {0}, {12}, {0,4}, ...  The same algebra as
+// ((10,4,13), (9,4,12)) with one erasure e_G = (G, xg) in a y-section G plus at most one
+// erasure e2 = (g2, x2) in one other section ({0}, {12}, {0,4}, ...), or two erasures in one
+// section and none elsewhere ({0,1}, {12,13}, ...).  The same algebra as
 // k_stream_local (stream_local.hpp: syndrome form, decode.rs:260-408, iscore order of
 // decode.rs:196-254), on the encode's LDS image (stream_encode.hpp) instead of 64-byte tiles.
 //
@@ -16,14 +17,15 @@
 //     C((G, b), z[G := X]).  Its own term folds into S_b; the coupled term is collected by its
 //     SOURCE: node (G, X) streamed at group b != X is the companion of node (G, b) at group X, so
 //     it adds A_(G,b)[r] C((G, X) @ b) to the presolved row r of group X (A_i = H_K^-1 gamma H_i,
-//     the tables the rounds use) -- for (G, b) used, or b = xg (the Out term of e_G).  Nothing of
+//     the tables the rounds use) -- for (G, b) used, or erased (its Out term).  Nothing of
 //     section G crosses groups in the bit-sliced domain, so a lane carries only S_b (32 registers)
 //     and the presolved rows C_r(group) (8 registers per erased row and group).
 //   * End of group b: C_r(b) += row e_r of H_K^-1 S_b (the presolve, byte domain).
 //   * After the four groups, the solve of k_stream_local with "slot" = group: (i) g2-lines of the
-//     groups != xg (lanes l ^ 8, l ^ 16: section g2's digit is at bits 0-1 of c), (ii) group xg:
-//     the dropped terms A_(G,A) C_eG(group A) of the used (G, A), in-lane, (iii) g2-lines of group
-//     xg.  Each step reads only values the previous steps finished.
+//     groups outside E_G (lanes l ^ 8, l ^ 16: section g2's digit is at bits 0-1 of c), (ii) the
+//     groups in E_G: the dropped terms A_(G,A) C_(G,g)(group A) of the used (G, A), in-lane,
+//     (iii) g2-lines of the groups in E_G, (iv) a both-erased pair of section G, in-lane.  Each
+//     step reads only values the previous steps finished.
 // The loader waves, the ring (a.ring - 1 node buffers streaming continuously across groups and
 // tiles; the tables in the last buffer) and the counted waits follow k_stream_local; the tile map
 // and the partial-tile handling (the piece straddling the end of an sc % 16 == 8 row rewritten
@@ -123,6 +125,14 @@ struct Local256 {
             for (int w = 0; w < 8; w++) v[w] |= C[k][gi][w] & m;
         }
     }
+    __device__ static void put(Rows &C, uint32_t r, int gi, const uint32_t (&v)[8]) {
+#pragma unroll
+        for (int k = 0; k < NE; k++) {
+            const uint32_t m = opq(r == uint32_t(k) ? 0xffffffffu : 0u);
+#pragma unroll
+            for (int w = 0; w < 8; w++) C[k][gi][w] = (C[k][gi][w] & ~m) | (v[w] & m);
+        }
+    }
     // C_r(group gi) ^= T_r * v for every erased row r
     __device__ static void add_mul(Rows &C, const uint8_t *tl, int tab0, const uint32_t (&v)[8], int gi) {
         GfTab tb[NE];
@@ -164,7 +174,7 @@ struct Local256 {
     // one step (group b, section Y): S_b += the section's terms; section G's coupled terms into C
     template <int Y>
     __device__ __forceinline__ static void step(const DecArgs &a, uint8_t *smem, uint32_t gbase, uint32_t R, uint32_t c,
-                                                uint32_t p, uint32_t b, uint32_t xg, uint32_t (&S)[32], Rows &C,
+                                                uint32_t p, uint32_t b, uint32_t eG, uint32_t (&S)[32], Rows &C,
                                                 const uint8_t *tl) {
         uint32_t alive_all = __builtin_amdgcn_readfirstlane(a.alive), used_all = __builtin_amdgcn_readfirstlane(a.used),
                  emY = __builtin_amdgcn_readfirstlane(a.emask[Y]);
@@ -217,7 +227,7 @@ struct Local256 {
         } else {
             // the coupled terms of group b's sources go to group X: coefficient A_(G,b)[r] when
             // (G, b) is used, or is e_G (its Out term); none from the red node (G, b) itself
-            const bool cross = ((used_all >> (4 * G + b)) & 1u) || b == xg;
+            const bool cross = (((used_all >> (4 * G)) | eG) >> b) & 1u;
             sfor<4>([&](auto xc) BS_INL {
                 constexpr int X = decltype(xc)::value;
                 constexpr int I = 4 * G + X;
@@ -297,7 +307,6 @@ __global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local25
     // ---------------- compute waves ----------------
     const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p0 = uint32_t(threadIdx.x) & 7u;
     const uint32_t eG = a.emask[G];
-    const uint32_t xg = uint32_t(__builtin_ctz(eG));
     const bool has2 = a.g2 >= 0;
     for (uint32_t k = 0; k < ntile; k++) {
         const StreamTile t = tm.tile(int(k), wslot, ns);
@@ -318,7 +327,7 @@ __global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local25
                 constexpr int Y = decltype(yc)::value;
                 lds_barrier();  // step (k, b, Y) landed
                 const uint8_t *tl = smem + R * BUF + opq(0u);
-                Kn::template step<Y>(a, smem, gb, R, opq(c0), opq(p0), b, xg, S, C, tl);
+                Kn::template step<Y>(a, smem, gb, R, opq(c0), opq(p0), b, eG, S, C, tl);
             });
             // end of group b: C_r(b) += row e_r of H_K^-1 S_b (bit planes -> bytes, then v_perm)
             const uint8_t *tl = smem + R * BUF + opq(0u);
@@ -355,35 +364,62 @@ __global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local25
         }
         const uint8_t *tl = smem + R * BUF + opq(0u);
         const uint32_t c = opq(c0), p = opq(p0);
-        // (i) g2-lines of the groups != xg (sources: level-0 values)
+        // (i) g2-lines of the groups outside E_G (sources: level-0 values)
         if (has2) {
             sfor<4>([&](auto gc) BS_INL {
                 constexpr int g = decltype(gc)::value;
-                if (uint32_t(g) != xg) Kn::line_g2(a, C, tl, c, g);
+                if (!((eG >> g) & 1u)) Kn::line_g2(a, C, tl, c, g);
             });
         }
-        // (ii) group xg: the in-lane terms of the used nodes (G, A), A != xg
+        // (ii) groups g in E_G: the in-lane terms of the used nodes (G, A), A not in E_G
         {
-            const uint32_t rg = uint32_t(a.rix[4 * G + xg]);
             const uint32_t used_all = a.used;
             sfor<4>([&](auto gc) BS_INL {
                 constexpr int g = decltype(gc)::value;
-                if (uint32_t(g) != xg) return;
+                if (!((eG >> g) & 1u)) return;
+                const uint32_t rg = uint32_t(a.rix[4 * G + g]);
                 sfor<4>([&](auto ac) BS_INL {
                     constexpr int A = decltype(ac)::value;
-                    if (A == g || !((used_all >> (4 * G + A)) & 1u)) return;
+                    if (((eG >> A) & 1u) || !((used_all >> (4 * G + A)) & 1u)) return;
                     uint32_t v[8];
                     Kn::get(C, rg, A, v);
                     Kn::add_mul(C, tl, 16 + (4 * G + A) * 4, v, g);
                 });
             });
         }
-        // (iii) red lanes of the g2-lines of group xg (sources final after (ii))
+        // (iii) red lanes of the g2-lines of the groups in E_G (sources final after (ii))
         if (has2) {
             sfor<4>([&](auto gc) BS_INL {
                 constexpr int g = decltype(gc)::value;
-                if (uint32_t(g) == xg) Kn::line_g2(a, C, tl, c, g);
+                if ((eG >> g) & 1u) Kn::line_g2(a, C, tl, c, g);
             });
+        }
+        // (iv) a both-erased pair of section G (two erasures there, none elsewhere): (G, x) at
+        // group g <-> (G, g) at group x, C = det^-1 (U + gamma U*) (transforms.rs:108-125)
+        if constexpr (NE == 2) {
+            if (__builtin_popcount(eG) == 2) {
+                const uint32_t gl = uint32_t(__builtin_ctz(eG)), xh = 31u - uint32_t(__builtin_clz(eG));
+                const uint32_t rx = uint32_t(a.rix[4 * G + xh]), rg = uint32_t(a.rix[4 * G + gl]);
+                const GfTab dinv = D::tab_at(tl, kDecDetInv);
+                sfor<4>([&](auto gc) BS_INL {
+                    constexpr int g = decltype(gc)::value;
+                    if (uint32_t(g) != gl) return;
+                    sfor<4>([&](auto xc) BS_INL {
+                        constexpr int x = decltype(xc)::value;
+                        if (x <= g || uint32_t(x) != xh) return;
+                        uint32_t u1[8], u2[8], c1[8], c2[8];
+                        Kn::get(C, rx, g, u1);  // (G, x) at group g
+                        Kn::get(C, rg, x, u2);  // (G, g) at group x
+#pragma unroll
+                        for (int w = 0; w < 8; w++) {
+                            c1[w] = gf_mul(u1[w] ^ gf_xt(u2[w]), dinv);
+                            c2[w] = gf_mul(u2[w] ^ gf_xt(u1[w]), dinv);
+                        }
+                        Kn::put(C, rx, g, c1);
+                        Kn::put(C, rg, x, c2);
+                    });
+                });
+            }
         }
         // outputs: pieces p and 8 + p of row (layer z) per erased row and group
         const bool full = t.vend >= t.b0 + uint32_t(Kn::W);

@@ -19,6 +19,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--what", default="decode4")
 ap.add_argument("--er", default="0,4,8,12", help="erasures of the decode (e.g. 0 for the local decode)")
+ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                help="back-to-back calls for this long first (the idle GPU's clock ramp; a trace "
+                     "summary then skips them: scripts/trace_summary.py --skip)")
 args = ap.parse_args()
 if args.what == "decode4":
     c = ClayCode(10, 4, 13)
@@ -38,7 +41,19 @@ else:
     hb = torch.randint(0, 256, (len(hs), len(info[0][1]) * sc), dtype=torch.uint8, device="cuda")
     out = torch.empty(chunk, dtype=torch.uint8, device="cuda")
     fn = lambda: c.repair_device(0, hs, [hb[i] for i in range(len(hs))], chunk, out)  # noqa: E731
+nwarm = 0
+if args.prewarm_ms > 0:
+    import time
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < args.prewarm_ms:
+        for _ in range(8):
+            fn()
+        nwarm += 8
+        torch.cuda.synchronize()
+    nwarm += 1
 for _ in range(args.iters):
     fn()
 torch.cuda.synchronize()
-print("done", args.what, args.iters)
+print("done", args.what, args.iters, "prewarm_calls", nwarm)

@@ -150,7 +150,7 @@ def _syndromes_presolved(code, C, E, used, rows):
 
 
 def presolved_by_source(code, C, E, used, rows, A, G):
-    """k_stream_local256's phase A (stream_local256.hpp) for one erased node in section G: per
+    """k_stream_local256's phase A (stream_local256.hpp) for one or two erased nodes in section G: per
     group b (digit G = b) S_b takes the sections != G as above and only the OWN terms H_i C(i, z)
     of section G; the coupled terms gamma H_(G,b) C((G, X), z[G := b]) of section G are collected
     by source -- node (G, X) at group b != X adds A_(G,b)[r] C((G, X), z') to row r at z'[G := X]

@@ -53,7 +53,7 @@ def stream_path(c, er):
         per = [0] * c.t
         for e in er:
             per[_internal(c, e) // c.q] += 1
-        return "stream-local256" if max(per) == 1 else "stream-local"
+        return "stream-local256" if max(per) == 1 or [n for n in per if n] == [2] else "stream-local"
     if fused2_eligible(c, er):
         return "stream-fused2"
     return None

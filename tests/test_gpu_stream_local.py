@@ -36,7 +36,8 @@ def local_path(c, er):
     per = [0] * c.t
     for e in er:
         per[_internal(c, e) // c.q] += 1
-    return "stream-local256" if max(per) == 1 else "stream-local"
+    busy = [n for n in per if n]
+    return "stream-local256" if max(per) == 1 or busy == [2] else "stream-local"
 
 
 def _local_patterns(c, seed, n3, n4):

@@ -66,7 +66,8 @@ def test_fused_rounds_algebra_matches_oracle(oracle_mod, k):
 @pytest.mark.parametrize("k", [10, 9])
 def test_local256_phase_a_by_source_matches(oracle_mod, k):
     """k_stream_local256's section-G terms collected by source give the same presolved rows as
-    the per-layer phase A, for every pattern with one erasure in its section plus at most one."""
+    the per-layer phase A, for every pattern with one erasure in its section plus at most one
+    more, and every pair of erasures in one section."""
     code = emu.Code(oracle_mod, k)
     rng = np.random.default_rng(k)
     sc = 3
@@ -76,11 +77,11 @@ def test_local256_phase_a_by_source_matches(oracle_mod, k):
         per = [0] * 4
         for e in er:
             per[code.internal(e) // 4] += 1
-        if max(per) != 1:
+        if not (max(per) == 1 or [n for n in per if n] == [2]):
             continue
         chunks = rng.integers(0, 256, (code.n, 256 * sc), dtype=np.uint8)
         C, E, used, rows, A = emu._setup(code, chunks, er)
-        G = code.internal(er[0]) // 4
+        G = max(range(4), key=lambda y: (per[y], -y))
         want = emu._syndromes_presolved(code, C, E, used, rows)
         got = emu.presolved_by_source(code, C, E, used, rows, A, G)
         assert np.array_equal(got, want), er
