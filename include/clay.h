@@ -198,7 +198,7 @@ int clay_decode_device(const clay_code_t *code, const uint8_t *const *chunks,
  * rebuilds the node with the repair of repair.rs:140-421 from the whole chunks (last exec path
  * "bs-repair-stream", when the sub-chunk gives every CU a tile): it reads only the alpha / q layers
  * of the node's repair plane (repair.rs:61-126) instead of every layer ((10,4,13) 1 GiB {0}:
- * 0.137 ms vs 0.386 on the local decode).  On a codeword the bytes equal decode.rs:31-161's (the
+ * 0.137 ms vs 0.350 on the local decode).  On a codeword the bytes equal decode.rs:31-161's (the
  * codeword through the k data chunks is unique); on chunks that are NOT one codeword they differ,
  * which is why clay_decode_device never takes this route.  Every other pattern runs exactly as
  * clay_decode_device.  The choice is an argument of the call, not process state: concurrent

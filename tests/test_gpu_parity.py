@@ -478,6 +478,47 @@ def test_cfg5_10_4_13_1GiB_decode_4_erasures_codeword_incl_parity(oracle_mod, to
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("er", [[0], [0, 4], [0, 1]])
+def test_local256_10_4_13_1GiB_decode(oracle_mod, torch_cuda, er):
+    """The local decode on 256-byte row runs at the BASELINE stripe (sc 419,432: partial tiles
+    ending at sc % 16 == 8) on random (non-codeword) chunks: every erased data chunk equals the
+    oracle's decode."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    chunk = 107_374_592
+    chunks = np.random.default_rng(17 + len(er)).integers(0, 256, (14, chunk), dtype=np.uint8)
+    av = {i: chunks[i] for i in range(14) if i not in er}
+    ref = np.frombuffer(o.decode(av, er), np.uint8).reshape(10, chunk)
+    full = torch.from_numpy(chunks).cuda()
+    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                    [outs[i] if i in er else None for i in range(14)], chunk)
+    torch.cuda.synchronize()
+    assert clay_amd.last_exec_path() == "stream-local256"
+    for e in er:
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
+
+
+@pytest.mark.slow
+def test_local256_10_4_13_1GiB_codeword_parity_pair(oracle_mod, torch_cuda):
+    """Two parity nodes of one section ({12, 13}: internal 14, 15, a both-erased pair) on a real
+    1 GiB codeword: both rebuilt parity chunks equal the encoded ones."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    ref = o.encode_array(rand_bytes(57, 1 << 30))
+    chunk = ref.shape[1]
+    er = [12, 13]
+    full = torch.from_numpy(ref).cuda()
+    outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(14)], er,
+                    [outs[i] if i in er else None for i in range(14)], chunk)
+    torch.cuda.synchronize()
+    assert clay_amd.last_exec_path() == "stream-local256"
+    for e in er:
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
+
+
+@pytest.mark.slow
 def test_cfg3_9_3_11_encode_full_size(oracle_mod, torch_cuda):
     """(9,3,11) stripe of 9 x 256 MiB: chunk 268,435,458, sc 3,314,018 (= 2 mod 8, off the
     bit-sliced kernels' 8-byte gate), whole parity against the oracle."""
