@@ -38,6 +38,8 @@ namespace bs {
 constexpr int kF2Iters[4] = {6, 4, 2, 1};
 constexpr int kF2Off[4] = {0, 6, 10, 12};
 constexpr int kF2Items = 13;
+template <int N>
+using IC = std::integral_constant<int, N>;
 
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
 // 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
@@ -164,6 +166,37 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 rb[kF2Off[y] + i] = zb * 64u + d8;
             }
         });
+        // ---- the round of iscore level LV + 1 of tile k - 1 (passes [I0, I1) of the lane's items):
+        // every target layer z of the level red in section Y adds sum over X != x_e(Y) of
+        // A_(Y,X) C(e_Y, z[Y := X]) (the three terms summed in registers, one 64-bit LDS atomic per
+        // row)
+        auto round = [&](auto lvc, auto i0c, auto i1c) BS_INL {
+            constexpr int LV = decltype(lvc)::value, I0 = decltype(i0c)::value, I1 = decltype(i1c)::value;
+#pragma unroll
+            for (int i = I0; i < I1; i++) {
+                const uint32_t ob = rb[kF2Off[LV] + i];
+                if (ob == ~0u) continue;
+                uint32_t acc[4][2] = {};
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
+                    const uint2 cv = *reinterpret_cast<const uint2 *>(src + ob + X * wy64);
+                    const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        acc[r][0] ^= gf_mul_idx(i0, tg[j][r]);
+                        acc[r][1] ^= gf_mul_idx(i1, tg[j][r]);
+                    }
+                }
+                const uint32_t oz = ob + xY * wy64;
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (uint32_t(r) < ne)  // the region holds ne rows
+                        __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + oz),
+                                               uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        };
         constexpr bool TM = (PROBE & 16) != 0;
         uint64_t tm_vm = 0, tm_bar = 0, tm_rnd = 0, tm_end = 0, t0 = 0;
         const uint64_t tm_start = TM ? __builtin_amdgcn_s_memtime() : 0;
@@ -191,33 +224,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 if (k == 0 || (PROBE & 1)) return;
                 // PROBE 64: the round at the compute waves' priority (the DMA issue above stays at 3)
                 if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(0);
-                // ---- round of iscore level y + 1 of tile k - 1: every target layer z of the level
-                // red in section Y adds sum over X != x_e(Y) of A_(Y,X) C(e_Y, z[Y := X]) (the three
-                // terms summed in registers, one 64-bit LDS atomic per row)
-#pragma unroll
-                for (int i = 0; i < kF2Iters[y]; i++) {
-                    const uint32_t ob = rb[kF2Off[y] + i];
-                    if (ob == ~0u) continue;
-                    uint32_t acc[4][2] = {};
-#pragma unroll
-                    for (int j = 0; j < 3; j++) {
-                        const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
-                        const uint2 cv = *reinterpret_cast<const uint2 *>(src + ob + X * wy64);
-                        const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            acc[r][0] ^= gf_mul_idx(i0, tg[j][r]);
-                            acc[r][1] ^= gf_mul_idx(i1, tg[j][r]);
-                        }
-                    }
-                    const uint32_t oz = ob + xY * wy64;
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        if (uint32_t(r) < ne)  // the region holds ne rows
-                            __hip_atomic_fetch_xor(reinterpret_cast<uint64_t *>(scr + uint32_t(r) * BUF + oz),
-                                                   uint64_t(acc[r][0]) | (uint64_t(acc[r][1]) << 32), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+                round(IC<y>{}, IC<0>{}, IC<kF2Iters[y]>{});
                 if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(3);
                 if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
             });
