@@ -1,7 +1,7 @@
 """numpy restatement of the streaming decodes' algebra (test infrastructure, CPU only).
 
-The HIP kernels k_stream_local (stream_local.hpp) and k_stream_fused2 / k_stream_solve
-(stream_fused2.hpp, stream_decode.hpp) decode q = 4, t = 4 codes in the syndrome form of the
+The HIP kernels k_stream_local (stream_local.hpp), k_stream_local256 (stream_local256.hpp) and
+k_stream_fused2 (stream_fused2.hpp, stream_decode.hpp) decode q = 4, t = 4 codes in the syndrome form of the
 reference's layered decode (decode.rs:167-408): per layer the RS reconstruct is the unique
 codeword through the first k+nu present shards, so the erased U values are H_K^-1 S with
 S = sum over used nodes of H_i U_i.  This module replays the kernels' step order on whole
@@ -263,7 +263,7 @@ def local_decode(code, chunks, erased_ext):
 
 
 def fused_decode(code, chunks, erased_ext):
-    """k_stream_solve / k_stream_fused2 (one erasure per y-section): presolve, then per iscore
+    """k_stream_fused2's rounds (one erasure per y-section): presolve, then per iscore
     level L >= 1 every layer of level L adds sum over its red sections Y and used X != x_e(Y) of
     A_(Y,X) C(e_Y, z[Y := X]) -- sources of level L - 1, final before the round."""
     C, E, used, rows, A = _setup(code, chunks, erased_ext)

@@ -437,26 +437,27 @@ def test_capture_arena_reclaimed(oracle_mod, torch_cuda):
         clay_amd.release_captured(0)
 
 
-@pytest.mark.parametrize("mode,path", [("grouped", "grouped"), ("auto", "stream-fused2")])
-def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda, mode, path):
-    """A 4-erasure (10,4,13) decode inside a stream capture, on the grouped executor (its U
-    workspace lease covered by the reserved workspace) and on the fused decode v2 (no workspace):
-    one eager call of the pattern prepared its tables, so the capture allocates nothing (the pool
-    does not grow) and replays bit-exact on new data.  A pattern never run before fails inside the
-    capture with a clear error instead of invalidating it."""
+@pytest.mark.parametrize("mode,path,er,er2", [("grouped", "grouped", [0, 4, 8, 12], [1, 5, 9, 13]),
+                                              ("auto", "stream-fused2", [0, 4, 8, 12], [1, 5, 9, 13]),
+                                              ("auto", "stream-local256", [0, 4], [1, 5])])
+def test_decode_graph_capture_after_prepare(oracle_mod, torch_cuda, mode, path, er, er2):
+    """A (10,4,13) decode inside a stream capture, on the grouped executor (its U workspace lease
+    covered by the reserved workspace), on the fused decode v2 and on the local decode on 256-byte
+    runs (no workspace): one eager call of the pattern prepared its tables, so the capture
+    allocates nothing (the pool does not grow) and replays bit-exact on new data.  A pattern never
+    run before fails inside the capture with a clear error instead of invalidating it."""
     prev = clay_amd.set_exec_mode(mode)
     try:
-        _decode_graph_capture(oracle_mod, torch_cuda, path)
+        _decode_graph_capture(oracle_mod, torch_cuda, path, er, er2)
     finally:
         clay_amd.set_exec_mode(prev)
 
 
-def _decode_graph_capture(oracle_mod, torch_cuda, path):
+def _decode_graph_capture(oracle_mod, torch_cuda, path, er, er2):
     torch = torch_cuda
     c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
     sc = 1024
     chunk = c.sub_chunk_no * sc
-    er = [0, 4, 8, 12]
     st = torch.cuda.Stream()
     clay_amd.release_captured(0)
     clay_amd.release_workspace(0)
@@ -482,7 +483,6 @@ def _decode_graph_capture(oracle_mod, torch_cuda, path):
         torch.cuda.synchronize()
         for e in er:
             assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (rep, e)
-    er2 = [1, 5, 9, 13]
     g2 = torch.cuda.CUDAGraph()
     with pytest.raises(clay_amd.DeviceError, match="not prepared"):
         with torch.cuda.graph(g2, stream=st):
