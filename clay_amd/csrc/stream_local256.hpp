@@ -40,7 +40,7 @@ namespace bs {
 template <int KD, int G, int NE>
 struct Local256 {
     using D = StreamDec<KD, G>;
-    static_assert(NE == 1 || NE == 2, "one erasure in section G plus at most one more");
+    static_assert(NE == 1 || NE == 2, "one or two erased rows");
     static constexpr int W = 256, CWAVES = 8, LOADERS = 4, BLOCK = 64 * (CWAVES + LOADERS);
     static constexpr int BUF = 16384;  // 64 columns x 256 B
     static constexpr int BPL = 16 / LOADERS;
