@@ -122,7 +122,9 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 10; i++) a.data[i] = data + i * chunk;
     for (int x = 0; x < 4; x++) a.par[x] = par + x * chunk;
     a.sc = sc;
-    a.tiles_per_xcd = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
+    // XCD region: sc / 8 rounded up to 32 bytes (the library's), or to argv[3] bytes (alignment A/B)
+    const uint32_t ralign = argc > 3 ? uint32_t(atoi(argv[3])) : 32u;
+    a.tiles_per_xcd = uint32_t(((sc + 7) / 8 + ralign - 1) / ralign * ralign);
     a.nslots = 32;
     const double bytes = 14.0 * chunk;
     auto rep = [&](const char *n, float ms) {
@@ -184,6 +186,17 @@ int main(int argc, char **argv) {
             rep("b2b L0 full (compute waves issue the DMA)", run_b2b<0, 0>(a, 200));
             rep("b2b L2 full", run_b2b<2, 0>(a, 200));
             rep("b2b math + stores, no DMA, no barriers", run_b2b<4, 2 | 65536>(a, 200));
+        }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'a') {  // alignment A/B: run with sc and region alignment from argv
+        printf("sc %u (row start mod 128 varies: %s), XCD region %u (alignment %u)\n", sc,
+               sc % 128 ? "yes" : "no, rows 128-aligned", a.tiles_per_xcd, ralign);
+        for (int rr = 0; rr < 2; rr++) {
+            rep("b2b full", run_b2b<4, 0>(a, 200));
+            rep("b2b memory only (DMA + stores)", run_b2b<4, 1>(a, 200));
+            rep("b2b stores only", run_b2b<4, 3>(a, 200));
+            rep("b2b reads only", run_b2b<4, 5>(a, 200));
         }
         return 0;
     }
