@@ -292,12 +292,20 @@ def small_stripe_rates(torch, dev, local, sh):
     return out
 
 
-def _event_times(torch, stream, fn, calls: int, warm: int = 10):
+def _event_times(torch, stream, fn, calls: int, warm: int = 10, prewarm_ms: float = 150.0):
     """HIP-event time of each of `calls` back-to-back calls on `stream` (events recorded on the
-    launch stream, all calls queued before one synchronize), after `warm` untimed calls."""
+    launch stream, all calls queued before one synchronize), after `warm` untimed calls and
+    untimed calls for `prewarm_ms` (the GPU idles while the previous leg's oracle check runs, and
+    an idle MI355X needs ~0.1 s of load to return to its sustained clock -- without this the
+    first leg after a check read 0.39 ms for a 0.35 ms kernel)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < prewarm_ms:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(calls)]
     for a, b in evs:
         a.record(stream)
@@ -327,7 +335,8 @@ def _slice_cols(arr2d, alpha, p0, w):
 
 
 def config_legs(torch, dev, local, stream, oracle_cls, calls: int):
-    """Driver-timed legs for the other BASELINE GPU configs,
+    """Driver-timed legs for the other BASELINE GPU configs (and
+    the single-erasure decode of config 5's stripe),
     each run AFTER the encode's timed region on fresh device buffers: HIP-event kernel time per
     call, the §8(d) algorithmic bytes, the fraction of 8 TB/s, the kernel path, and a column-slice
     check against the oracle (every byte offset of the sub-chunks is an independent codeword, so
@@ -363,6 +372,21 @@ def config_legs(torch, dev, local, stream, oracle_cls, calls: int):
     algo = (c.n - len(er)) * chunk + sum(1 for e in er if e < 10) * chunk
     out["decode_cfg5"] = _leg("(k=10,m=4,d=13) decode, 1 GiB stripe, erasures {0,4,8,12}, random chunks",
                               ms, algo, path, ok, {"bytes_counted": "10 survivors read + 3 erased data chunks written"})
+    # the same stripe with one erasure {0} (the common case: the local decode on 256-byte runs)
+    er = [0]
+    ins = [None if i in er else full[i] for i in range(c.n)]
+    ous = [outs[i] if i in er else None for i in range(c.n)]
+    ms = _event_times(torch, stream, lambda: c.decode_device(ins, er, ous, chunk, local, sh), calls)
+    path = clay_amd.last_exec_path()
+    ok = True
+    for p0 in (0, sc - VERIFY_W):
+        s = _slice_cols(full, alpha, p0, VERIFY_W)
+        got = _slice_cols(outs, alpha, p0, VERIFY_W)
+        ref = np.frombuffer(o.decode({i: s[i] for i in range(c.n) if i not in er}, er), np.uint8).reshape(10, -1)
+        ok = ok and np.array_equal(got[0], ref[0])
+    algo = (c.n - 1) * chunk + chunk
+    out["decode_1erasure"] = _leg("(k=10,m=4,d=13) decode, 1 GiB stripe, erasure {0}, random chunks",
+                                  ms, algo, path, ok, {"bytes_counted": "13 survivors read + 1 erased data chunk written"})
     del full, outs, ins, ous
 
     # config 3: (9,3,11) repair of node 0 from d = 11 helpers, chunk 268,435,458 (beta sub-chunks each)
