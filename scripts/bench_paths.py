@@ -154,6 +154,8 @@ if __name__ == "__main__":
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "grouped")),
             ("cfg5", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),  # under CLAY_EXEC
+            ("cfg2", lambda: decode_cfg(4, 2, 5, 64 << 20, [0])),  # under CLAY_EXEC
+            ("cfg2", lambda: decode_cfg(4, 2, 5, 64 << 20, [5])),
             # the fused decode v2 for 3 and 2 erasures in distinct sections (auto: split / local)
             ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8], "stream-fused2")),
             ("f2x", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8])),
