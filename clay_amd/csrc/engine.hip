@@ -1755,12 +1755,16 @@ static Error encode_device_impl(const clay_code_t *code, const uint8_t *const *d
 // (per_sec_max: the most erasures one y-section may hold).
 template <int KD>
 static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const *cout, const std::vector<uint8_t> &erased,
-                       size_t sc, int per_sec_max, bs::DecArgs &a, std::vector<uint32_t> &tabs, bool *ok) {
+                       size_t sc, int per_sec_max, bs::DecArgs &a, std::vector<uint32_t> &tabs, bool *ok,
+                       bool any_sc = false) {
     *ok = false;
     const clay_code_t &c = cs.code;
     using S = bs::Shape<KD, 4>;
     if (int(c.k) != KD || c.m != 4 || c.q != 4 || c.t != 4 || c.q * c.t != 16) return Error{};
-    if (sc % 8 || sc < 512 || double(S::ALPHA) * double(sc) >= 4294967296.0) return Error{};
+    // any_sc (k_stream_local256: LDS-DMA and 16-byte stores at any byte alignment, partial pieces
+    // patched / stored byte by byte): any sub-chunk >= 512 and any chunk alignment; the other
+    // streaming decodes need 8-byte rows
+    if ((!any_sc && sc % 8) || sc < 512 || double(S::ALPHA) * double(sc) >= 4294967296.0) return Error{};
     const GF &gf = GF::get();
     std::vector<int> E;
     int per_sec[4] = {0, 0, 0, 0};
@@ -1773,6 +1777,7 @@ static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const 
     for (int y = 0; y < 4; y++)
         if (per_sec[y] > per_sec_max) return Error{};
     for (int i = 0; i < 16; i++) {
+        if (any_sc) continue;
         if (cin[i] && reinterpret_cast<uintptr_t>(cin[i]) % 8) return Error{};
         if (cout[i] && reinterpret_cast<uintptr_t>(cout[i]) % 8) return Error{};
     }
@@ -1877,6 +1882,8 @@ static Error dec_tables(CodeState &cs, const DevProps &prop, const std::vector<u
 
 hipError_t launch_stream_local_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
 hipError_t launch_stream_local256_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_local256.hip
+hipError_t launch_stream_local256_any_kernel(int kd, int g, const bs::DecArgs &a, hipStream_t stream,
+                                             int dev);  // decode_local256_any.hip
 
 // Local decode (stream_local.hpp): erasures in one y-section G (any number) plus at most one
 // erasure in one other section g2 -- every iscore dependency inside a wave, one launch, no
@@ -1900,10 +1907,14 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
             if (per_sec[y] > 1) return Error{};  // two sections with several erasures: rounds needed
             g2 = y;
         }
+    // one erasure in section G plus at most one in g2, or two in G and none elsewhere: the
+    // 256-byte-run kernel (stream_local256.hpp), which also takes sub-chunks that are not a
+    // multiple of 8
+    const bool w256 = (per_sec[G] == 1 || (per_sec[G] == 2 && g2 < 0)) && !tuning().local_w64;
     bs::DecArgs a;
     std::vector<uint32_t> tabs;
     bool ok = false;
-    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 4, a, tabs, &ok);
+    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 4, a, tabs, &ok, w256);
     if (e || !ok) return e;
     // column digits: section g2 (if any) at bits 0-1, the others above in section order
     {
@@ -1915,10 +1926,7 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
     if (g2 >= 0) a.x2 = uint32_t(__builtin_ctz(a.emask[g2]));
     perm_table(gamma_det_inv(), &tabs[bs::kDecDetInv * 8]);  // (1 + gamma^2)^-1, transforms.rs:108-125
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));
-    // one erasure in section G plus at most one in g2, or two in G and none elsewhere: the
-    // 256-byte-run kernel (stream_local256.hpp), XCD regions of whole 32-byte units and 256-byte
-    // tiles as the encode's
-    const bool w256 = (per_sec[G] == 1 || (per_sec[G] == 2 && g2 < 0)) && !tuning().local_w64;
+    // the 256-byte-run kernel: XCD regions of whole 32-byte units and 256-byte tiles as the encode's
     if (w256) {
         a.region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
         a.nslots = std::min(per_xcd, std::max(1u, (a.region + 255u) / 256u));
@@ -1928,7 +1936,14 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
     e = dec_tables(cs, prop, tabs, stream, &a.tabs);
     if (e) return e;
     if (w256) {
-        CLAY_HIP(launch_stream_local256_kernel(KD, G, a, stream, prop.dev));
+        // rows of 8-byte multiples at 8-byte-aligned chunks: the 8-byte kernel; else the ANY one
+        bool any = sc % 8 != 0;
+        for (int i = 0; i < 16; i++) {
+            any = any || (cin[i] && reinterpret_cast<uintptr_t>(cin[i]) % 8);
+            any = any || (cout[i] && reinterpret_cast<uintptr_t>(cout[i]) % 8);
+        }
+        if (any) CLAY_HIP(launch_stream_local256_any_kernel(KD, G, a, stream, prop.dev));
+        else CLAY_HIP(launch_stream_local256_kernel(KD, G, a, stream, prop.dev));
         t_last_exec = "stream-local256";
     } else {
         CLAY_HIP(launch_stream_local_kernel(KD, G, a, stream, prop.dev));

@@ -28,8 +28,9 @@
 //     step reads only values the previous steps finished.
 // The loader waves, the ring (a.ring - 1 node buffers streaming continuously across groups and
 // tiles; the tables in the last buffer) and the counted waits follow k_stream_local; the tile map
-// and the partial-tile handling (the piece straddling the end of an sc % 16 == 8 row rewritten
-// in LDS after landing) follow k_stream_encode.
+// and the partial-tile handling (the piece straddling the end of a row rewritten in LDS after
+// landing) follow k_stream_encode; any sub-chunk >= 512 (rows at any byte alignment: LDS-DMA and
+// the 16-byte stores take any alignment, the partial pieces are patched and stored byte by byte).
 #pragma once
 
 #include "stream_decode.hpp"
@@ -37,7 +38,11 @@
 namespace clay {
 namespace bs {
 
-template <int KD, int G, int NE>
+// ANY: sub-chunks that are not multiples of 8 (rows at any byte alignment): the partial pieces
+// are shifted into place in LDS and stored byte by byte; the ANY = false instantiation keeps the
+// 8-byte tail handling (a separate kernel: the byte paths, though cold, slowed the 8-byte-row
+// kernel by 28 % when compiled into it)
+template <int KD, int G, int NE, bool ANY = false>
 struct Local256 {
     using D = StreamDec<KD, G>;
     static_assert(NE == 1 || NE == 2, "one or two erased rows");
@@ -95,18 +100,44 @@ struct Local256 {
             for (int j = 0; j < BPL; j++) dma16(lds_buf + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
         }
     }
-    // sc % 16 == 8 tile end: the straddling piece of every row holds 8 valid bytes; rewrite it
-    // in LDS from global memory once the step's DMA has landed
+    // a tile end inside a 16-byte piece: the DMA read the straddling piece of every row from
+    // vend - 16 (issue()); once it has landed, rewrite it with its nv = vend - pos valid bytes at
+    // the piece's start: ANY = false (nv = 8, sc % 16 == 8) from global memory; ANY = true (any nv)
+    // by a funnel shift of the landed bytes by 16 - nv in LDS
     __device__ static void patch(const DecArgs &a, const Loader &L, uint8_t *buf, const uint8_t *node, StreamTile t,
                                  uint32_t b, int lane) {
         const uint32_t sc = uint32_t(a.sc), pos = t.b0 + L.k16;
         if (!(pos < t.vend && pos + 16u > t.vend)) return;
+        if constexpr (!ANY) {
 #pragma unroll
-        for (int j = 0; j < BPL; j++) {
-            const int blk = L.li * BPL + j;
-            const uint64_t o = uint64_t(L.off[j] - L.k16) + uint64_t(b * D::wt(G)) * sc + pos;
-            const uint2 gv = *reinterpret_cast<const uint2 *>(node + o);
-            *reinterpret_cast<uint4 *>(buf + blk * 1024 + lane * 16) = make_uint4(gv.x, gv.y, 0u, 0u);
+            for (int j = 0; j < BPL; j++) {
+                const int blk = L.li * BPL + j;
+                const uint64_t o = uint64_t(L.off[j] - L.k16) + uint64_t(b * D::wt(G)) * sc + pos;
+                const uint2 gv = *reinterpret_cast<const uint2 *>(node + o);
+                *reinterpret_cast<uint4 *>(buf + blk * 1024 + lane * 16) = make_uint4(gv.x, gv.y, 0u, 0u);
+            }
+        } else {
+            const uint32_t sh = 16u - (t.vend - pos);  // bytes to drop at the front: 1..15
+            const uint32_t ws = sh >> 2, bs = (sh & 3u) * 8u;
+#pragma unroll
+            for (int j = 0; j < BPL; j++) {
+                uint4 *q = reinterpret_cast<uint4 *>(buf + (L.li * BPL + j) * 1024 + lane * 16);
+                const uint4 v = *q;
+                const uint32_t d[5] = {v.x, v.y, v.z, v.w, 0u};
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    // words k + ws and k + ws + 1 of d (0 past the end), selected without indexing d
+                    uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+                    for (int m = 0; m < 4; m++) {
+                        lo = (k + m < 5 && ws == uint32_t(m)) ? d[k + m < 5 ? k + m : 4] : lo;
+                        hi = (k + m + 1 < 5 && ws == uint32_t(m)) ? d[k + m + 1 < 5 ? k + m + 1 : 4] : hi;
+                    }
+                    o[k] = bs ? ((lo >> bs) | (hi << (32u - bs))) : lo;
+                }
+                *q = make_uint4(o[0], o[1], o[2], o[3]);
+            }
         }
     }
 
@@ -247,9 +278,9 @@ struct Local256 {
 
 // grid = 8 * nslots (one workgroup per CU); LDS = 10 x 16 KiB: a ring of a.ring - 1 node
 // buffers and the tables (presolve, A_i) in the last.  a.region: XCD region bytes (multiple of 32).
-template <int KD, int G, int NE>
-__global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local256(DecArgs a) {
-    using Kn = Local256<KD, G, NE>;
+template <int KD, int G, int NE, bool ANY = false>
+__global__ __launch_bounds__((Local256<KD, G, NE, ANY>::BLOCK)) void k_stream_local256(DecArgs a) {
+    using Kn = Local256<KD, G, NE, ANY>;
     using D = typename Kn::D;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -461,11 +492,21 @@ __global__ __launch_bounds__((Local256<KD, G, NE>::BLOCK)) void k_stream_local25
                     for (int h = 0; h < 2; h++) {
                         const uint32_t pos = t.b0 + 16u * p + 128u * uint32_t(h);
                         const uint32_t nv = pos >= t.vend ? 0u : (t.vend - pos >= 16u ? 16u : t.vend - pos);
-                        if (nv == 16u)
-                            *reinterpret_cast<uint4 *>(row + 128 * h) =
-                                make_uint4(C[r][g][4 * h], C[r][g][4 * h + 1], C[r][g][4 * h + 2], C[r][g][4 * h + 3]);
-                        else if (nv >= 8u)
-                            *reinterpret_cast<uint2 *>(row + 128 * h) = make_uint2(C[r][g][4 * h], C[r][g][4 * h + 1]);
+                        const uint32_t w0 = C[r][g][4 * h], w1 = C[r][g][4 * h + 1], w2 = C[r][g][4 * h + 2],
+                                       w3 = C[r][g][4 * h + 3];
+                        if (nv == 16u) {
+                            *reinterpret_cast<uint4 *>(row + 128 * h) = make_uint4(w0, w1, w2, w3);
+                        } else if constexpr (ANY) {
+                            // the row's last bytes (any count: sub-chunks need not be multiples of 8)
+#pragma unroll 1
+                            for (uint32_t i = 0; i < nv; i++) {
+                                const uint32_t q = i >> 2;
+                                const uint32_t wv = q == 0u ? w0 : q == 1u ? w1 : q == 2u ? w2 : w3;
+                                row[128 * h + int(i)] = uint8_t(wv >> (8u * (i & 3u)));
+                            }
+                        } else if (nv >= 8u) {
+                            *reinterpret_cast<uint2 *>(row + 128 * h) = make_uint2(w0, w1);
+                        }
                     }
                 }
             }

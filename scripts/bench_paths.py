@@ -176,6 +176,8 @@ if __name__ == "__main__":
             ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [12])),
             ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4])),
             ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1])),
+            ("local", lambda: decode_cfg(9, 4, 12, 1 << 30, [0])),
+            ("local", lambda: decode_cfg(9, 4, 12, 1 << 30, [0, 4])),
             # clay_decode_device_codeword: one erasure rebuilt by the repair kernel from whole
             # chunks (charged the repair route's bytes)
             ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [0], codeword=True)),

@@ -134,3 +134,36 @@ def test_local_decode_matches_grouped_incl_parity(oracle_mod, torch_cuda, er):
         clay_amd.set_exec_mode(prev)
     for e in er:
         assert np.array_equal(a[e], b[e]), e
+
+
+@pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
+@pytest.mark.parametrize("sc", [513, 515, 1037, 64 * 37 + 42])
+def test_local256_any_subchunk(oracle_mod, torch_cuda, cfg, sc):
+    """k_stream_local256 at sub-chunks that are not multiples of 8 (rows at odd byte offsets:
+    the (9,4,12) 1 GiB stripe has sc = 2 mod 8), for every 1-erasure pattern and the 2-erasure
+    patterns it takes, on random chunks vs the oracle; the other local patterns fall back to the
+    plan executors there (the 64-byte kernel needs 8-byte rows)."""
+    torch = torch_cuda
+    c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc * 3 + cfg[0])
+    pats = [[e] for e in range(c.n)] + [list(p) for p in itertools.combinations(range(c.n), 2)][::3]
+    pats += [[0, 1, 4]]
+    n256 = 0
+    for er in pats:
+        chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+        got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
+        path = clay_amd.last_exec_path()
+        if local_eligible(c, er) and local_path(c, er) == "stream-local256":
+            assert path == "stream-local256", (er, path)
+            n256 += 1
+        else:
+            assert not path.startswith("stream-local"), (er, path)
+        av = {i: chunks[i] for i in range(c.n) if i not in er}
+        ref = np.frombuffer(o.decode(av, er), dtype=np.uint8).reshape(c.k, -1)
+        for e in er:
+            if e < c.k:
+                assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e, path)
+            else:
+                assert np.all(got[e] == 0xA5), "parity output written though not requested"
+    assert n256 > 10
