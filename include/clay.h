@@ -285,12 +285,13 @@ int clay_set_encode_path(int mode);
  *   0 auto    -- the tile-fused executor (one launch, U workspace in LDS) for small plans
  *                (<= 32 op groups) whose U slots fit the LDS budget, else the grouped
  *                per-level executor; for q = 4, t = 4 codes ((10,4,13), (9,4,12)) with
- *                sc % 8 == 0, sc >= 512: decodes whose erasures lie in one y-section plus at
- *                most one erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4}, {0,1,2,3},
- *                ...) run a single-launch local decode: one erasure in its section plus
- *                at most one more ({0}, {12}, {0,4}) on 256-byte row runs (k_stream_local256,
- *                last path "stream-local256"), the others on 64-byte tiles (k_stream_local,
- *                "stream-local"); 3 or 4 erasures in distinct y-sections (the BASELINE
+ *                sc >= 512: decodes whose erasures lie in one y-section plus at most one
+ *                erasure in one other section ({0}, {0,4}, {0,1}, {0,1,4}, {0,1,2,3}, ...) run
+ *                a single-launch local decode: one erasure in its section plus at most one
+ *                more, or two in one section ({0}, {12}, {0,4}, {0,1}), on 256-byte row runs
+ *                (k_stream_local256, last path "stream-local256", any sub-chunk), the others
+ *                on 64-byte tiles (k_stream_local, "stream-local", sc % 8 == 0); 3 or 4
+ *                erasures in distinct y-sections (sc % 8 == 0; the BASELINE
  *                {0,4,8,12} included) the fused decode v2 (k_stream_fused2, "stream-fused2")
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
