@@ -33,8 +33,10 @@ struct DecArgs {
     uint32_t csh[4];
     int32_t g2;
     uint32_t x2;
-    // k_stream_fused2: per section y, the phase-A copy (StreamDec::phase_a): x (0..3) = node (y, x)
-    // erased and every other node used, 4 = none erased and all used, -1 = the run-time copy
+    // per section y, the phase-A copy (StreamDec::phase_a of k_stream_fused2, Local256::step):
+    // x (0..3) = node (y, x) erased and every other node used, 4 = none erased and all used,
+    // 5 / 6 = none erased, all alive and only node 0 / nodes 0-1 used (k_stream_local256 only),
+    // -1 = the run-time copy
     int32_t scase[4];
 };
 // local decode: v_perm table of det^-1 = (1 + gamma^2)^-1 (pair inversion, transforms.rs:108-125)

@@ -1849,6 +1849,10 @@ static Error dec_setup(CodeState &cs, const uint8_t *const *cin, uint8_t *const 
         const uint32_t em = a.emask[y], un = (used >> (4 * y)) & 15u, al = (a.alive >> (4 * y)) & 15u;
         const bool ok1 = __builtin_popcount(em) <= 1 && un == (~em & 15u) && al == (~em & ~shortn & 15u);
         a.scase[y] = ok1 ? (em ? __builtin_ctz(em) : 4) : -1;
+        // k_stream_local256 (one erased row): no erasure, every node alive and only node 0 / nodes
+        // 0-1 used (the ignored nodes of one erasure: the last present ones); the fused decode
+        // takes the run-time copy for these
+        if (!ok1 && em == 0 && al == (~shortn & 15u) && (un == 1u || un == 3u)) a.scase[y] = un == 1u ? 5 : 6;
     }
     if (nt == 0) return Error{};
     // the local kernel streams through R - 1 buffers (the last holds tables): a step's

@@ -202,14 +202,33 @@ struct Local256 {
         }
     }
 
-    // one step (group b, section Y): S_b += the section's terms; section G's coupled terms into C
-    template <int Y>
+    // one step (group b, section Y): S_b += the section's terms; section G's coupled terms into C.
+    // SC >= 0 (NE = 1): the section's structure at compile time (DecArgs::scase: node (Y, SC)
+    // erased and every other node used for SC < 4; none erased, all alive and all / only node 0 /
+    // nodes 0-1 used for SC = 4 / 5 / 6); SC = -1: the run-time masks
+    template <int Y, int SC = -1>
     __device__ __forceinline__ static void step(const DecArgs &a, uint8_t *smem, uint32_t gbase, uint32_t R, uint32_t c,
                                                 uint32_t p, uint32_t b, uint32_t eG, uint32_t (&S)[32], Rows &C,
                                                 const uint8_t *tl) {
+        constexpr bool CT = SC >= 0;
+        if constexpr (CT) {
+            // a distinct marker opens and closes every copy, and the lane constants are opaque per
+            // copy: no code is hoisted above or sunk below the caller's switch
+            asm volatile("; local256 step copy %0 begin" ::"i"(SC));
+            c = opq(c);
+            p = opq(p);
+        }
+        constexpr uint32_t kEm = (CT && SC < 4) ? 1u << SC : 0u;
+        constexpr uint32_t kUsed = !CT ? 0u : SC <= 4 ? (~kEm & 15u) : SC == 5 ? 1u : 3u;
+        constexpr uint32_t kAlive = 15u & ~D::short_nib(Y) & ~kEm;
         uint32_t alive_all = __builtin_amdgcn_readfirstlane(a.alive), used_all = __builtin_amdgcn_readfirstlane(a.used),
                  emY = __builtin_amdgcn_readfirstlane(a.emask[Y]);
         asm volatile("" : "+s"(alive_all), "+s"(used_all), "+s"(emY));
+        if constexpr (CT) {
+            alive_all = kAlive << (4 * Y);
+            used_all = kUsed << (4 * Y);
+            emY = kEm;
+        }
         const uint32_t aliveY = (alive_all >> (4 * Y)) & 15u;
         const uint32_t rs = a.sec_off[Y];
         auto buf_of = [&](uint32_t x) BS_INL {  // node (Y, x) buffer (x alive)
@@ -272,6 +291,31 @@ struct Local256 {
                 }
                 __builtin_amdgcn_sched_barrier(0);
             });
+        }
+        if constexpr (CT) asm volatile("; local256 step copy %0 end" ::"i"(SC));
+    }
+    // the step's copy for a.scase[Y] (one erased row only: with two the copies' registers spill)
+    template <int Y>
+    __device__ __forceinline__ static void step_any(const DecArgs &a, uint8_t *smem, uint32_t gbase, uint32_t R,
+                                                    uint32_t c, uint32_t p, uint32_t b, uint32_t eG, uint32_t (&S)[32],
+                                                    Rows &C, const uint8_t *tl) {
+        if constexpr (NE != 1) {
+            step<Y>(a, smem, gbase, R, c, p, b, eG, S, C, tl);
+        } else if constexpr (Y == G) {
+            switch (a.scase[Y]) {
+            case 0: step<Y, 0>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            case 1: step<Y, 1>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            case 2: step<Y, 2>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            case 3: step<Y, 3>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            default: step<Y>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            }
+        } else {
+            switch (a.scase[Y]) {
+            case 4: step<Y, 4>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            case 5: step<Y, 5>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            case 6: step<Y, 6>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            default: step<Y>(a, smem, gbase, R, c, p, b, eG, S, C, tl); break;
+            }
         }
     }
 };
@@ -358,7 +402,7 @@ __global__ __launch_bounds__((Local256<KD, G, NE, ANY>::BLOCK)) void k_stream_lo
                 constexpr int Y = decltype(yc)::value;
                 lds_barrier();  // step (k, b, Y) landed
                 const uint8_t *tl = smem + R * BUF + opq(0u);
-                Kn::template step<Y>(a, smem, gb, R, opq(c0), opq(p0), b, eG, S, C, tl);
+                Kn::template step_any<Y>(a, smem, gb, R, opq(c0), opq(p0), b, eG, S, C, tl);
             });
             // end of group b: C_r(b) += row e_r of H_K^-1 S_b (bit planes -> bytes, then v_perm)
             const uint8_t *tl = smem + R * BUF + opq(0u);
