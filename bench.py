@@ -6,7 +6,7 @@ One step = encode of one 1 GiB stripe (the reference's ClayCode::encode of
 whose data chunks are already resident in HBM; parity (4 chunks) is written to
 HBM.  Multi-GPU: one process per GPU, each rank encodes its own stripe (stripes
 are independent, encode.rs:30-80 -> no data-path collective; weak scaling).  The
-barrier / max-time reduction are timing plumbing only.
+barrier / max-time reduction are timing plumbing only and run over gloo (no RCCL).
 
     python bench.py                      # N = 1
     python bench.py --gpus 8             # spawns 8 ranks itself (no torchrun needed)
@@ -74,8 +74,8 @@ def parse(argv=None):
                     help="torch.distributed timeout (s) for init and collectives")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher tests
     ap.add_argument("--cpu-dry", action="store_true",
-                    help="test mode without a GPU: the oracle replaces the device encode, gloo "
-                         "replaces RCCL; everything else (launcher, ranks, timing, JSON) is the same")
+                    help="test mode without a GPU: the oracle replaces the device encode; everything "
+                         "else (launcher, ranks, gloo timing plane, JSON) is the same")
     return ap.parse_args(argv)
 
 
@@ -433,7 +433,14 @@ def config_legs(torch, dev, local, stream, oracle_cls, calls: int):
     ous = [outs[i] if i in er else None for i in range(c.n)]
     ms_d = _event_times(torch, stream, lambda: c.decode_device(ins, er, ous, chunk, local, sh), calls)
     dpath = clay_amd.last_exec_path()
-    ok_d = bool(torch.equal(outs[0], full[0]))  # a codeword: the erased chunk comes back exactly
+    # oracle check on column slices, as the other legs (the survivors' slices through the
+    # oracle's decode; ADVICE r05: not a self-consistency check against our own encode)
+    ok_d = True
+    for p0 in (0, sc - VERIFY_W):
+        s = _slice_cols(full, alpha, p0, VERIFY_W)
+        got = _slice_cols(outs, alpha, p0, VERIFY_W)
+        ref = np.frombuffer(o.decode({i: s[i] for i in range(c.n) if i not in er}, er), np.uint8).reshape(4, -1)
+        ok_d = ok_d and np.array_equal(got[0], ref[0])
     out["cfg2_encode"] = _leg("(k=4,m=2,d=5) encode, 64 MiB stripe", ms_e, 6 * chunk, epath, ok_e,
                               {"bytes_counted": "4 data chunks read + 2 parity written"})
     out["cfg2_decode"] = _leg("(k=4,m=2,d=5) decode of erasure {0}, 64 MiB stripe (a codeword)", ms_d,
@@ -474,8 +481,10 @@ def run_rank(args) -> int:
             print(f"bench: LOCAL_RANK {local} but only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
             return 2
     if world > 1:
-        dist.init_process_group("gloo" if args.cpu_dry else "nccl",
-                                timeout=datetime.timedelta(seconds=args.dist_timeout))
+        # gloo in every mode: the data path has no collective (whole stripes per GPU), and the
+        # control plane -- the start / stop barrier and the all_gather of three doubles per rank
+        # -- needs no RCCL bring-up across the node (north_star: "RCCL unused")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
     from oracle import oracle  # checker / CPU legs only (and the dry run's stand-in encode)
     oracle.build()
 
@@ -550,7 +559,7 @@ def run_rank(args) -> int:
 
     # per-rank wall / kernel mean / verified -> every rank (max over ranks is the job time)
     mine = torch.tensor([el, float(np.mean(kern_ms)), 0.0 if verified is False else 1.0],
-                        dtype=torch.float64, device=dev_t)
+                        dtype=torch.float64)  # CPU tensor: the gloo group carries it
     if world > 1:
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)

@@ -38,19 +38,19 @@ static float run(BsArgs a, int reps) {
 
 // steady state: n back-to-back launches between one pair of events (what bench.py and the
 // profiler see); mean per launch
-template <int L, int PROBE>
-static float run_b2b(BsArgs a, int n) {
+template <int L, int PROBE, int MAP = 0>
+static float run_b2b(BsArgs a, int n, int warm = 50) {
     using Kn = StreamEnc<10, L>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_stream_encode<10, L, PROBE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_stream_encode<10, L, PROBE, MAP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, Kn::LDS_BYTES);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    for (int i = 0; i < 50; i++)
-        k_stream_encode<10, L, PROBE><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
+    for (int i = 0; i < warm; i++)
+        k_stream_encode<10, L, PROBE, MAP><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
     (void)hipEventRecord(e0);
     for (int i = 0; i < n; i++)
-        k_stream_encode<10, L, PROBE><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
+        k_stream_encode<10, L, PROBE, MAP><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES>>>(a);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -66,7 +66,7 @@ static float run_b2b(BsArgs a, int n) {
 // Segment timing (PROBE 4096, stream_encode.hpp TimeAcc): per-workgroup s_memtime sums of the
 // last of `n` back-to-back launches, then one single launch timed with events to convert cycles
 // to time.  Prints per-tile averages over the workgroups and the start / end spread.
-template <int TP>
+template <int TP, int MAP = 0>
 static void timing_report(BsArgs a, int n) {
     using Kn = StreamEnc<10, 4>;
     const int grid = int(a.nslots) * 8;
@@ -75,8 +75,8 @@ static void timing_report(BsArgs a, int n) {
     (void)hipMalloc(&tb, rec * 8);
     (void)hipMemset(tb, 0, rec * 8);
     a.par[4] = reinterpret_cast<uint8_t *>(tb);
-    const float ms_plain = run_b2b<4, 0>(a, n);
-    const float ms_tm = run_b2b<4, TP>(a, n);
+    const float ms_plain = run_b2b<4, 0, MAP>(a, n);
+    const float ms_tm = run_b2b<4, TP, MAP>(a, n);
     std::vector<uint64_t> h(rec);
     (void)hipMemcpy(h.data(), tb, rec * 8, hipMemcpyDeviceToHost);
     printf("b2b ms: plain %.4f  timing-probe %.4f (s_memtime counts per XCD; cycles below are per tile)\n", ms_plain, ms_tm);
@@ -174,19 +174,63 @@ int main(int argc, char **argv) {
         return 0;
     }
     if (argc > 2 && argv[2][0] == 'v') {  // steady-state variants: which parts add
+        // live = SINK probes (stream_encode.hpp PROBE 262144): the end-of-group work runs and the
+        // parity stores become XORs into a sink, so the math cannot be deleted (the
+        // round-5 "no stores" variants 4 / 6 compiled to 4 / 3 v_bitop3 and timed nothing)
         printf("sc %u variants, back-to-back (200 launches after 50 untimed)\n", sc);
         for (int rr = 0; rr < 3; rr++) {
             rep("b2b full", run_b2b<4, 0>(a, 200));
-            rep("b2b no parity stores (math + DMA)", run_b2b<4, 4>(a, 200));
-            rep("b2b memory only (DMA + stores)", run_b2b<4, 1>(a, 200));
-            rep("b2b math + stores (no DMA)", run_b2b<4, 2>(a, 200));
-            rep("b2b math only", run_b2b<4, 6>(a, 200));
+            rep("b2b memory only (DMA + stores, no math)", run_b2b<4, 1>(a, 200));
             rep("b2b reads only", run_b2b<4, 5>(a, 200));
             rep("b2b stores only", run_b2b<4, 3>(a, 200));
-            rep("b2b L0 full (compute waves issue the DMA)", run_b2b<0, 0>(a, 200));
-            rep("b2b L2 full", run_b2b<2, 0>(a, 200));
+            rep("b2b live reads + math (no stores)", run_b2b<4, 262144>(a, 200));
+            rep("b2b live math only (no DMA, no stores)", run_b2b<4, 262146>(a, 200));
+            rep("b2b math + stores (no DMA)", run_b2b<4, 2>(a, 200));
             rep("b2b math + stores, no DMA, no barriers", run_b2b<4, 2 | 65536>(a, 200));
+            rep("b2b live math only, no barriers", run_b2b<4, 262146 | 65536>(a, 200));
         }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'n') {  // round-6 lane map (MAP 1: light section 2 on waves 4-7; MAP 2: on 0-3)
+        printf("sc %u lane map A/B, back-to-back (200 launches after 50 untimed)\n", sc);
+        if (argv[2][1] == 't') {  // segment timing of both maps
+            timing_report<4096, 0>(a, 200);
+            printf("---- map 1\n");
+            timing_report<4096, 1>(a, 200);
+            return 0;
+        }
+        for (int rr = 0; rr < 3; rr++) {
+            rep("b2b full, map 0 (round 5)", run_b2b<4, 0, 0>(a, 200));
+            rep("b2b full, map 1 (light waves 4-7)", run_b2b<4, 0, 1>(a, 200));
+            rep("b2b full, map 2 (light waves 0-3)", run_b2b<4, 0, 2>(a, 200));
+            rep("b2b live math only, map 0", run_b2b<4, 262146, 0>(a, 200));
+            rep("b2b live math only, map 1", run_b2b<4, 262146, 1>(a, 200));
+            rep("b2b math + stores, map 1", run_b2b<4, 2, 1>(a, 200));
+            rep("b2b memory only, map 1", run_b2b<4, 1, 1>(a, 200));
+            rep("b2b live reads + math, map 1", run_b2b<4, 262144, 1>(a, 200));
+        }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'w') {  // the 'v' variants, 10 launches each (for one rocprofv3 --pmc pass)
+        rep("full", run_b2b<4, 0>(a, 10, 2));
+        rep("memory only", run_b2b<4, 1>(a, 10, 2));
+        rep("reads only", run_b2b<4, 5>(a, 10, 2));
+        rep("stores only", run_b2b<4, 3>(a, 10, 2));
+        rep("live reads + math", run_b2b<4, 262144>(a, 10, 2));
+        rep("live math only", run_b2b<4, 262146>(a, 10, 2));
+        rep("math + stores", run_b2b<4, 2>(a, 10, 2));
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'f') {  // the no-barrier timing probe, bounds-checked
+        unsigned int *flag;
+        (void)hipMalloc(&flag, 4);
+        (void)hipMemset(flag, 0, 4);
+        a.par[5] = reinterpret_cast<uint8_t *>(flag);
+        printf("sc %u no-barrier timing probe (PROBE 4096|65536|2) with bounds checks (524288)\n", sc);
+        timing_report<4096 | 65536 | 2 | 524288>(a, 50);
+        unsigned int h = 0;
+        (void)hipMemcpy(&h, flag, 4, hipMemcpyDeviceToHost);
+        printf("bounds flags 0x%x (bits 0-3 parity store of node X, 4-7 ragged store, 8 compute record, 9 loader record)\n", h);
         return 0;
     }
     if (argc > 2 && argv[2][0] == 'a') {  // alignment A/B: run with sc and region alignment from argv

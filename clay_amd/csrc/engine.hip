@@ -578,6 +578,13 @@ static bool capturing(hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
+// id of the capture `st` is in (0: none)
+static unsigned long long capture_id(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(st, &cs, &id) != hipSuccess || cs != hipStreamCaptureStatusActive) return 0;
+    return id;
+}
 
 // A pooled device buffer (U workspaces, host-API staging).  A lease is handed to one
 // call at a time; on release an event is recorded on the caller's stream, and the
@@ -590,6 +597,11 @@ struct Lease {
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;  // stream of the last use (reuse there needs no event query)
     bool used = false, busy = false, pinned = false;
+    // taken by a call inside a stream capture: the capturing stream and its capture id, so
+    // clay_release_captured can refuse while that capture is still open
+    bool captured = false;
+    hipStream_t cap_st = nullptr;
+    unsigned long long cap_id = 0;
 };
 // A batched launch's device pointer table, cached by content (immutable once
 // uploaded, so concurrent users may share it); freed LRU after its users' events.
@@ -601,6 +613,8 @@ struct PtrTable {
     uint64_t last = 0;
     int users = 0;  // calls between ptr_table() and ptr_table_done(): never freed meanwhile
     bool pinned = false;
+    hipStream_t cap_st = nullptr;  // captured tables: the capturing stream and its capture id
+    unsigned long long cap_id = 0;
 };
 constexpr size_t kMaxPtrTables = 64;
 constexpr size_t kCapArena = size_t(4) << 20;  // pointer tables created inside stream captures
@@ -755,6 +769,11 @@ static Error lease_acquire(DevState &ds, size_t bytes, hipStream_t st, Lease **o
     // stream whose work is still running (free when that work is complete)
     if (best->used && !cap) CLAY_HIP(hipStreamWaitEvent(st, best->ev, 0));
     best->busy = true;
+    if (cap) {
+        best->captured = true;
+        best->cap_st = st;
+        best->cap_id = capture_id(st);
+    }
     *out = best;
     return Error{};
 }
@@ -825,6 +844,8 @@ static Error ptr_table(DevState &ds, const std::vector<uint8_t *> &tab, hipStrea
             return make_error(CLAY_ERR_DEVICE, ds.cap_used, bytes, 0, "pointer-table arena for captured calls exhausted");
         auto t = std::make_unique<PtrTable>();
         t->pinned = true;
+        t->cap_st = st;
+        t->cap_id = capture_id(st);
         t->d = ds.cap_d + ds.cap_used;
         t->h = ds.cap_h + ds.cap_used;
         ds.cap_used += bytes;
@@ -2083,9 +2104,10 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     size_t n_erased = 0;
     for (size_t in = 0; in < tn; in++) n_erased += erased[in] && !(in >= c.k && in < c.k + c.nu) ? 1 : 0;
     // clay_decode_device_codeword (the caller vouches, for this call only, that the chunks are one
-    // codeword): a single erasure is rebuilt by the repair kernel; every other decode runs as
-    // clay_decode_device does
-    if (codeword && n_erased == 1 && ner == 1 && ids.size() + 1 == c.n) {
+    // codeword): a single erasure is rebuilt by the repair kernel under the exec modes that pick
+    // the bit-sliced repair kernels (auto, "stream": as repair_device_impl); every other decode,
+    // and every decode under "grouped" / "tile" (A/B runs), runs as clay_decode_device does
+    if (codeword && (xmode == kExecAuto || xmode == kExecStream) && n_erased == 1 && ner == 1 && ids.size() + 1 == c.n) {
         bool done = false;
         e = decode_by_repair(c, chunks, er[0], outs[er[0]], chunk, dev, static_cast<hipStream_t>(stream), &done);
         if (e || done) return e;
@@ -2580,19 +2602,26 @@ int clay_release_captured(int device, clay_error_t *err) {
     // capture mode, torch.cuda.graph's default) would invalidate that capture.  The caller has
     // waited for every replay of the graphs and destroyed them (clay.h); refuse while one of this
     // library's calls is inside a capture right now (its table or lease is in use).
+    // A lease taken inside a capture is refused back while that call runs (busy) or while the
+    // capture it was taken in is still open (its graph does not exist yet, so the caller cannot
+    // have destroyed it): unpinning it then would hand a graph-owned workspace to the next eager
+    // call.  Pointer tables likewise, by their capture's stream and id.
     std::lock_guard<std::mutex> lk(ds->mu);
     for (auto &t : ds->captured)
-        if (t->users > 0)
+        if (t->users > 0 || (t->cap_id && capture_id(t->cap_st) == t->cap_id))
             return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "a stream capture is using the pointer-table arena"), err);
     for (auto &l : ds->pool)
-        if (l->pinned && l->busy)
+        if (l->captured && (l->busy || (l->cap_id && capture_id(l->cap_st) == l->cap_id)))
             return report(make_error(CLAY_ERR_DEVICE, 0, 0, 0, "a stream capture is using a pooled workspace"), err);
     ds->captured.clear();
     ds->cap_used = 0;
     for (auto &l : ds->pool)
-        if (l->pinned && !l->busy) {
-            l->pinned = false;
+        if (l->pinned) {
+            // the caller has waited for every replay (clay.h): no event guards this buffer now
+            l->pinned = l->captured = false;
             l->used = false;
+            l->cap_st = nullptr;
+            l->cap_id = 0;
         }
     return 0;
 }

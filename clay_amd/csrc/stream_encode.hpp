@@ -100,8 +100,14 @@ struct ChipMap {
 };
 
 // CPL / CPS: cache policy of the LDS-DMA loads / parity stores (0 default, 1 nt, 2 sc1);
-// CSE: RS folds through compile-time common subexpressions (xor_cse.hpp)
-template <int KD, int LOADERS, int CPL = 0, int CPS = 0, bool CSE = true>
+// CSE: RS folds through compile-time common subexpressions (xor_cse.hpp);
+// SINK (probe builds only): every parity store is replaced by an XOR of its data into a per-lane
+// sink, so the math stays live without the stores (bench_tools/stream_probe "live" variants)
+// MAP: compute-lane map (0: column c = 8 * wave + (lane >> 3), round 5; 1: the round-6 map below,
+// digit 2 of c per wave so that section 2's work is wave-uniform, the light waves 4-7; 2: the same
+// with the light waves 0-3, for A/B)
+template <int KD, int LOADERS, int CPL = 0, int CPS = 0, bool CSE = true, bool SINK = false, bool CHECK = false,
+          int MAP = 0>
 struct StreamEnc {
     using K6 = EncMath<KD>;
     using S = typename K6::S;
@@ -138,22 +144,51 @@ struct StreamEnc {
     // exactly those pairs, so own and companion reads are bank-conflict free (companions of
     // sections 0/1 keep c mod 4; section 2's companion row is shared = broadcast).
     __host__ __device__ static constexpr uint32_t sw(uint32_t r) { return ((r >> 1) & 1u) * 8u; }
+    // Round-6 map (MAP 1 / 2).  Compute lane (wave w, lane l): part p = l & 7, in-lane column index
+    // k = l >> 3 = column bits 2-4 (digit 1 and the low bit of digit 0), the wave supplies digit 2
+    // (bits 0-1) and bit 5.  Digit 2 per wave makes section 2 wave-uniform: for d2 in {2, 3} the
+    // PRT companions of nodes 8, 9 are the shortened nodes 10, 11 (zero), so U = C for 8 and 9 and
+    // U = 0 for 10 and 11 -- a light section-2 step of two plain node folds (section_light).
+    // MAP 1 puts d2 in {2, 3} on waves 4-7 (the younger wave of each SIMD, the one that loses the
+    // VALU arbitration); MAP 2 on waves 0-3.  The LDS image is swizzled per node and row,
+    // piece k of row r of node (Y, x) at slot k ^ swn(x, r), swn = 8 (bit 3 of r ^ bit 1 of x):
+    // own and companion reads of every section step stay bank-conflict free
+    // (bench_tools/lds_conflicts.py models both maps: 0 extra cycles).  The DPP store pair is
+    // columns c, c ^ 4 (lane bit 3 = column bit 2): rows z and z + 16.
+    static constexpr uint32_t PAIR = MAP == 0 ? 4u : 16u;  // row distance of the DPP store pair
+    __device__ static int colmap(int w, int k) {
+        if constexpr (MAP == 0) return 8 * w + k;
+        const int hi = MAP == 1 ? ((w >> 2) & 1) : (((w >> 2) & 1) ^ 1);
+        return (w & 1) | (hi << 1) | (k << 2) | (((w >> 1) & 1) << 5);
+    }
+    __device__ static bool light_wave(int w) { return MAP == 1 ? w >= 4 : (MAP == 2 ? w < 4 : false); }
+    __host__ __device__ static constexpr uint32_t swn(uint32_t x, uint32_t r) {
+        return MAP == 0 ? sw(r) : ((((r >> 3) & 1u) ^ ((x >> 1) & 1u))) * 8u;
+    }
 
     // ---------------- loader ----------------
     struct Loader {
-        uint32_t off[BPL];  // per block: lane offset in its node chunk for g = 0, b0 = 0
-        uint32_t k16;       // 16 x the piece this lane fetches in every block
+        // per block and node class b = bit 1 of the section-local node index (MAP 1 / 2 swizzle;
+        // MAP 0: both the same): lane offset in its node chunk for g = 0, b0 = 0
+        uint32_t off[2][BPL];
         uint32_t rl;        // row-in-block of this lane
+        uint32_t slot;      // 16-byte LDS slot this lane fills in every block
         int li;
     };
+    // 16 x the piece lane L fetches in block j of a node of class b
+    __device__ static uint32_t k16_of(const Loader &L, int j, uint32_t b) {
+        const uint32_t r = uint32_t(L.li * BPL + j) * 4u + L.rl;
+        return (L.slot ^ swn(b * 2u, r)) * 16u;
+    }
     __device__ static void loader_init(Loader &L, uint32_t sc, int li, int lane) {
         L.li = li;
         L.rl = uint32_t(lane) >> 4;
-        L.k16 = ((uint32_t(lane) & 15u) ^ sw(L.rl)) * 16u;
+        L.slot = uint32_t(lane) & 15u;
 #pragma unroll
         for (int j = 0; j < BPL; j++) {
             const uint32_t r = uint32_t(li * BPL + j) * 4u + L.rl;
-            L.off[j] = r * 4u * sc + L.k16;
+            L.off[0][j] = r * 4u * sc + k16_of(L, j, 0u);
+            L.off[1][j] = r * 4u * sc + k16_of(L, j, 1u);
         }
     }
     // DMA of step (section Y, group g) of tile t into section Y's node buffers
@@ -165,19 +200,23 @@ struct StreamEnc {
             constexpr int x = decltype(xc)::value;
             constexpr int node = Y * Q + x;
             if constexpr (node < KD) {
+                constexpr uint32_t b = (uint32_t(x) >> 1) & 1u;
                 const uint32_t dst = lds0 + uint32_t(node * NODE_BYTES) + uint32_t(L.li * BPL) * 1024u;
                 if (full) {
                     const uint8_t *base = uniform_ptr(a.data[node] + (uint64_t(g) * sc + t.b0));
 #pragma unroll
-                    for (int j = 0; j < BPL; j++) dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[j]);
+                    for (int j = 0; j < BPL; j++) dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[b][j]);
                 } else {
                     // partial tile: a piece straddling vend is read from vend - 16 (patched
                     // after landing), a piece wholly past vend from b0 (never used)
                     const uint8_t *base = uniform_ptr(a.data[node] + uint64_t(g) * sc);
-                    uint32_t pos = t.b0 + L.k16;
-                    if (pos + 16u > t.vend) pos = t.vend - 16u;  // past vend: unused; vend = sc >= 16
 #pragma unroll
-                    for (int j = 0; j < BPL; j++) dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[j] - L.k16 + pos);
+                    for (int j = 0; j < BPL; j++) {
+                        const uint32_t k16 = k16_of(L, j, b);
+                        uint32_t pos = t.b0 + k16;
+                        if (pos + 16u > t.vend) pos = t.vend - 16u;  // past vend: unused; vend = sc >= 16
+                        dma16p<CPL>(dst + uint32_t(j) * 1024u, base, L.off[b][j] - k16 + pos);
+                    }
                 }
             }
         });
@@ -193,14 +232,14 @@ struct StreamEnc {
     template <int Y>
     __device__ static void patch(const BsArgs &a, const Loader &L, uint8_t *smem, StreamTile t, int g, int lane) {
         const uint32_t sc = uint32_t(a.sc);
-        const uint32_t pos = t.b0 + L.k16;
-        if (!(pos < t.vend && pos + 16u > t.vend)) return;
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
             constexpr int node = Y * Q + x;
             if constexpr (node < KD) {
 #pragma unroll
                 for (int j = 0; j < BPL; j++) {
+                    const uint32_t pos = t.b0 + k16_of(L, j, (uint32_t(x) >> 1) & 1u);
+                    if (!(pos < t.vend && pos + 16u > t.vend)) continue;
                     const int blk = L.li * BPL + j;
                     const uint32_t layer = (uint32_t(blk) * 4u + L.rl) * 4u + uint32_t(g);
                     const uint2 gv = *reinterpret_cast<const uint2 *>(a.data[node] + uint64_t(layer) * sc + pos);
@@ -227,6 +266,25 @@ struct StreamEnc {
     };
     __device__ static LaneS lane_consts(int c, int part) {
         LaneS L;
+        if constexpr (MAP != 0) {
+            // own: row c, slot p ^ swn(x, c); the node's bit-1 term swaps the two pieces (load_x)
+            const uint32_t uc = uint32_t(c), up = uint32_t(part);
+            L.own[0] = uc * 256u + ((up ^ (((uc >> 3) & 1u) * 8u)) * 16u);
+            L.own[1] = L.own[0] ^ 128u;
+#pragma unroll
+            for (int y = 0; y < 3; y++) {
+                const int sh = dshift(y);
+                L.cy[y] = (c >> sh) & 3;
+                const uint32_t cy = uint32_t(L.cy[y]);
+                const uint32_t row0 = (uc & ~(3u << sh)) * 256u + cy * uint32_t(NODE_BYTES);
+                // companion row c' = c[y := x]: bit 3 of c' is c's for y = 0, 2 and x's for y = 1
+                // (the x term then swaps the pieces, load_x)
+                const uint32_t rb = y == 1 ? 0u : ((uc >> 3) & 1u);
+                L.cb[y][0] = row0 + ((up ^ ((rb ^ ((cy >> 1) & 1u)) * 8u)) * 16u);
+                L.cb[y][1] = L.cb[y][0] ^ 128u;
+            }
+            return L;
+        }
         const uint32_t pk = (uint32_t(part) ^ sw(uint32_t(c))) * 16u;
         L.own[0] = uint32_t(c) * 256u + pk;
         L.own[1] = L.own[0] ^ 128u;
@@ -252,6 +310,24 @@ struct StreamEnc {
     // own value and companion of node x of section Y (zero for shortened nodes)
     template <int Y, int X>
     __device__ static void load_x(const uint8_t *slot, const LaneS &L, uint32_t (&o)[8], uint32_t (&cv)[8]) {
+        if constexpr (MAP != 0) {
+            constexpr int bx = (X >> 1) & 1;
+            if constexpr (Y * Q + X < KD) {
+                read32(slot + X * NODE_BYTES + L.own[bx], slot + X * NODE_BYTES + L.own[bx ^ 1], o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) o[w] = 0;
+            }
+            if ((Y * Q + L.cy[Y]) < KD) {
+                constexpr uint32_t step = uint32_t(256) << dshift(Y);
+                constexpr int hb = Y == 1 ? bx : 0;
+                read32(slot + L.cb[Y][hb] + X * step, slot + L.cb[Y][hb ^ 1] + X * step, cv);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; w++) cv[w] = 0;
+            }
+            return;
+        }
         if constexpr (Y * Q + X < KD) {
             read32(slot + X * NODE_BYTES + L.own[0], slot + X * NODE_BYTES + L.own[1], o);
         } else {
@@ -305,6 +381,25 @@ struct StreamEnc {
         });
     }
 
+    // Section 2 on a light wave (MAP 1 / 2, digit 2 of every lane's column in {2, 3}): the
+    // companions of nodes 8 and 9 are shortened (zero), so U = C (transforms.rs:42-55 with C* = 0)
+    // and the shortened nodes' U are zero (no fold); no companion reads, no PRT.
+    template <int SBN = 1>
+    __device__ __forceinline__ static void section_light(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
+        static_assert(MAP != 0, "wave-uniform digit 2");
+        sfor<Q>([&](auto xc) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            if constexpr (2 * Q + x < KD) {
+                constexpr int bx = (x >> 1) & 1;
+                uint32_t u[8];
+                read32(slot + x * NODE_BYTES + L.own[bx], slot + x * NODE_BYTES + L.own[bx ^ 1], u);
+                if constexpr (CSE) K6::template fold_x_cse<2, x>(u, acc);
+                else K6::template fold_x<2, x>(u, acc);
+                if constexpr (SBN > 0) __builtin_amdgcn_sched_barrier(0);
+            }
+        });
+    }
+
     // ---------------- compute: outputs ----------------
     // Parity C (8 planes) -> bytes -> HBM at parity node X, layer z = 4c + G.  A lane holds
     // pieces p and 8 + p of its row; lanes c and c ^ 1 (lane ^ 8, same row of 16 lanes) swap
@@ -312,8 +407,27 @@ struct StreamEnc {
     // 256-byte row runs (even columns, then odd columns) instead of 8 rows x 128 B.
     template <int X>
     __device__ __forceinline__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, StreamTile t, uint32_t prel,
-                               bool ragged) {
+                               bool ragged, uint32_t &sink) {
         transpose8(cv);
+        if (SINK && !ragged) {
+            const bool odd = (threadIdx.x >> 3) & 1u;
+            uint32_t r[4], lo[4], hi[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t send = odd ? cv[i] : cv[4 + i];
+                r[i] = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, false));
+                lo[i] = odd ? r[i] : cv[i];
+                hi[i] = odd ? cv[4 + i] : r[i];
+            }
+            sink ^= xor3(xor3(lo[0], lo[1], lo[2]), xor3(lo[3], hi[0], hi[1]), hi[2] ^ hi[3]);
+            sink += X;  // keeps the per-output order visible (no cancellation across outputs)
+            return;
+        }
+        if (SINK) {
+            sink ^= xor3(xor3(cv[0], cv[1], cv[2]), xor3(cv[3], cv[4], cv[5]), cv[6] ^ cv[7]);
+            return;
+        }
+        (void)sink;
         if (!ragged) {
             const bool odd = (threadIdx.x >> 3) & 1u;
             uint32_t r[4], lo[4], hi[4];
@@ -324,18 +438,32 @@ struct StreamEnc {
                 lo[i] = odd ? r[i] : cv[i];      // row of the even column, piece (odd ? 8 : 0) + p
                 hi[i] = odd ? cv[4 + i] : r[i];  // row of the odd column
             }
-            uint32_t off = (z - (odd ? 4u : 0u)) * uint32_t(a.sc);
+            uint32_t off = (z - (odd ? PAIR : 0u)) * uint32_t(a.sc);
             asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
             off += t.b0 + prel + (odd ? 128u : 0u);
             const uint8_t *base = uniform_ptr(a.par[X]);  // SGPR base (also under the probes' deferred flow)
+            if constexpr (CHECK) {
+                // probe bounds check (stream_probe "f"): flag and skip a store outside par[X]
+                const uint64_t lim = uint64_t(a.sc) * 256u;
+                if (uint64_t(off) + 16u > lim || uint64_t(off) + PAIR * a.sc + 16u > lim) {
+                    atomicOr(reinterpret_cast<unsigned int *>(a.par[5]), 1u << X);
+                    return;
+                }
+            }
             st16sp<CPS>(base, off, lo[0], lo[1], lo[2], lo[3]);
-            st16sp<CPS>(base, off + 4u * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
+            st16sp<CPS>(base, off + PAIR * uint32_t(a.sc), hi[0], hi[1], hi[2], hi[3]);
         } else {
             uint8_t *p = a.par[X] + uint64_t(z) * a.sc + t.b0 + prel;
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const uint32_t pos = t.b0 + prel + 128u * uint32_t(h);
                 const uint32_t nv = pos >= t.vend ? 0u : (t.vend - pos >= 16u ? 16u : t.vend - pos);
+                if constexpr (CHECK) {
+                    if (nv && (z >= 256u || pos + nv > a.sc)) {
+                        atomicOr(reinterpret_cast<unsigned int *>(a.par[5]), 16u << X);
+                        continue;
+                    }
+                }
                 if (nv == 16u)
                     *reinterpret_cast<uint4 *>(p + 128 * h) = make_uint4(cv[4 * h], cv[4 * h + 1], cv[4 * h + 2], cv[4 * h + 3]);
                 else if (nv >= 8u)
@@ -348,12 +476,12 @@ struct StreamEnc {
     // (several instantiations in one translation unit), acc and Hold would go through scratch.
     template <int G>
     __device__ __forceinline__ static void end_group(const BsArgs &a, const uint32_t (&acc)[Q * 8], typename K6::Hold &H, int c,
-                                     StreamTile t, uint32_t prel, bool ragged) {
+                                     StreamTile t, uint32_t prel, bool ragged, uint32_t &sink) {
         const uint32_t zg = uint32_t(c * 4 + G);
         uint32_t cv[8];
 #pragma unroll
         for (int w = 0; w < 8; w++) cv[w] = acc[G * 8 + w];
-        put<G>(a, cv, zg, t, prel, ragged);
+        put<G>(a, cv, zg, t, prel, ragged, sink);
         auto pair = [&](const uint32_t *uh_at_g, const uint32_t *ug_at_h, auto hc) BS_INL {
             constexpr int h = decltype(hc)::value;
             const uint32_t zh = uint32_t(c * 4 + h);
@@ -376,8 +504,8 @@ struct StreamEnc {
                 c1[w] = c12[w];
                 c2[w] = c12[8 + w];
             }
-            put<h>(a, c1, zg, t, prel, ragged);  // C[h][z_G]
-            put<G>(a, c2, zh, t, prel, ragged);  // C[G][z_h]
+            put<h>(a, c1, zg, t, prel, ragged, sink);  // C[h][z_G]
+            put<G>(a, c2, zh, t, prel, ragged, sink);  // C[G][z_h]
         };
         auto keep = [&](int ri, int p) BS_INL {
 #pragma unroll
@@ -413,7 +541,14 @@ struct StreamEnc {
 // outputs are stored at the end of group g is (g + slot) % 4 (store bursts desynchronised
 // across workgroups; only meaningful with bit 1), 2048 = chip round-robin tile map (ChipMap),
 // 4096 = s_memtime segment timing (TimeAcc), 8192 = a group's end work after the next barrier,
-// 16384 / 32768 = no scheduling barrier between nodes / one after every two nodes.
+// 16384 / 32768 = no scheduling barrier between nodes / one after every two nodes,
+// 262144 = SINK (StreamEnc): the end-of-group work runs in full but every parity store becomes an
+// XOR into a per-lane sink, stored once at the end under a run-time predicate the compiler cannot
+// fold -- the live-math "no stores" variants (262144: reads + math; 262146: math only);
+// 524288 = CHECK (probe): every parity store and timing record is bounds-checked, a violation is
+// flagged in a.par[5] (atomicOr of a bit per kind) and the access skipped.  Bit 4
+// (no end-of-group work at all) lets the compiler delete the math and is kept only as a record
+// of that (PROBE 4 / 6 compiled to 4 / 3 v_bitop3).
 // Segment timing of the probe instantiations (PROBE bit 4096): s_memtime cycles summed per
 // kind (compute wave: 0 barrier wait, 1 section math; loader wave: 0 vmcnt wait, 1 barrier,
 // 2 DMA issue) and per section y, plus the end-of-group work (outputs) per group g; written by
@@ -450,9 +585,11 @@ struct TimeAcc {
     }
 };
 
-template <int KD, int LOADERS, int PROBE = 0>
+template <int KD, int LOADERS, int PROBE = 0, int MAP = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
-    using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3, ((PROBE >> 10) & 1) == 0>;
+    using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3, ((PROBE >> 10) & 1) == 0, (PROBE & 262144) != 0,
+                         (PROBE & 524288) != 0, MAP>;
+    uint32_t sink = 0;  // SINK probes only
     constexpr bool TM = (PROBE & 4096) != 0;
     using K6 = typename Kn::K6;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -512,7 +649,12 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         }
         if constexpr (TM) {
             T.t_end = __builtin_amdgcn_s_memtime();
-            if (lane == 0) T.put(reinterpret_cast<uint64_t *>(a.par[4]) + (blockIdx.x * 12u + uint32_t(wave)) * 24u, ntile);
+            const uint32_t rec = blockIdx.x * 12u + uint32_t(wave);
+            if ((PROBE & 524288) != 0 && (rec >= gridDim.x * 12u || wave >= 12)) {
+                if (lane == 0) atomicOr(reinterpret_cast<unsigned int *>(a.par[5]), 512u);
+            } else if (lane == 0) {
+                T.put(reinterpret_cast<uint64_t *>(a.par[4]) + rec * 24u, ntile);
+            }
         }
         return;
     }
@@ -520,7 +662,8 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
     if constexpr ((PROBE & 16) != 0) {
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
-    const int c = int(threadIdx.x) >> 3, part = int(threadIdx.x) & 7;
+    const int c = Kn::colmap(wave, (int(threadIdx.x) >> 3) & 7), part = int(threadIdx.x) & 7;
+    const bool light = Kn::light_wave(wave);
     const uint32_t prel = uint32_t(part) * 16u;
     uint32_t acc[Kn::Q * 8];
     typename K6::Hold H;
@@ -542,10 +685,10 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
     StreamTile pt{0, 0};
     auto end_any = [&](int ge, StreamTile t) BS_INL {
         const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
-        if (ge == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged);
-        else if (ge == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged);
-        else if (ge == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged);
-        else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged);
+        if (ge == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged, sink);
+        else if (ge == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged, sink);
+        else if (ge == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged, sink);
+        else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged, sink);
     };
     TimeAcc T;
     T.t_start = TM ? __builtin_amdgcn_s_memtime() : 0;
@@ -590,7 +733,14 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         typename Kn::LaneS L = LC;
         asm volatile("" : "+v"(L.own[0]), "+v"(L.own[1]), "+v"(L.cb[0][0]), "+v"(L.cb[0][1]));
         asm volatile("" : "+v"(L.cb[1][0]), "+v"(L.cb[1][1]), "+v"(L.cb[2][0]));
-        asm volatile("" : "+v"(L.cy[0]), "+v"(L.cy[1]), "+v"(L.cy[2]));
+        if constexpr (MAP != 0) {
+            // digit 2 is wave-uniform: cy[2] lives in an SGPR (the VGPR goes to cb[2][1])
+            asm volatile("" : "+v"(L.cb[2][1]));
+            asm volatile("" : "+v"(L.cy[0]), "+v"(L.cy[1]));
+            L.cy[2] = __builtin_amdgcn_readfirstlane(L.cy[2]);
+        } else {
+            asm volatile("" : "+v"(L.cy[0]), "+v"(L.cy[1]), "+v"(L.cy[2]));
+        }
         if constexpr ((PROBE & 1) != 0) {
             if (s == 0)
 #pragma unroll
@@ -600,7 +750,9 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             constexpr bool BAL = (PROBE & 131072) != 0;
             if (y == 0) Kn::template section<0, SBN, BAL>(smem, L, acc);
             else if (y == 1) Kn::template section<1, SBN, BAL>(smem + Kn::REGION, L, acc);
-            else Kn::template section<2, SBN, BAL>(smem + 2 * Kn::REGION, L, acc);
+            else if (MAP != 0 && light) {
+                if constexpr (MAP != 0) Kn::template section_light<SBN>(smem + 2 * Kn::REGION, L, acc);
+            } else Kn::template section<2, SBN, BAL>(smem + 2 * Kn::REGION, L, acc);
         }
         if constexpr (TM) T.add(1, y, t0);
         if (y == 2 && !(PROBE & 4)) {
@@ -625,9 +777,18 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
     if constexpr (DEFER) {
         if (pend >= 0) end_any(pend, pt);
     }
+    if constexpr ((PROBE & 262144) != 0) {
+        // a.sdata is 0 in the probe: the predicate is (almost) never true, but not foldable
+        if (sink == uint32_t(a.sdata) + 0x9E3779B9u) a.par[0][threadIdx.x] = uint8_t(sink);
+    }
     if constexpr (TM) {
         T.t_end = __builtin_amdgcn_s_memtime();
-        if (lane == 0) T.put(reinterpret_cast<uint64_t *>(a.par[4]) + (blockIdx.x * 12u + uint32_t(wave)) * 24u, ntile);
+        const uint32_t rec = blockIdx.x * 12u + uint32_t(wave);
+        if ((PROBE & 524288) != 0 && (rec >= gridDim.x * 12u || wave >= 12)) {
+            if (lane == 0) atomicOr(reinterpret_cast<unsigned int *>(a.par[5]), 256u);
+        } else if (lane == 0) {
+            T.put(reinterpret_cast<uint64_t *>(a.par[4]) + rec * 24u, ntile);
+        }
     }
 }
 

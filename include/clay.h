@@ -202,7 +202,9 @@ int clay_decode_device(const clay_code_t *code, const uint8_t *const *chunks,
  * codeword through the k data chunks is unique); on chunks that are NOT one codeword they differ,
  * which is why clay_decode_device never takes this route.  Every other pattern runs exactly as
  * clay_decode_device.  The choice is an argument of the call, not process state: concurrent
- * clay_decode_device calls are unaffected.  No reference counterpart (decode.rs has one path). */
+ * clay_decode_device calls are unaffected.  The repair route is taken under exec modes auto and
+ * "stream" only (as clay_repair_device's kernel choice); under "grouped" / "tile" the call runs
+ * as clay_decode_device.  No reference counterpart (decode.rs has one path). */
 int clay_decode_device_codeword(const clay_code_t *code, const uint8_t *const *chunks,
                                 const size_t *erasures, size_t n_erasures, uint8_t *const *out_chunks,
                                 size_t chunk_size, int device, void *stream, clay_error_t *err);
@@ -246,11 +248,13 @@ int clay_release_workspace(int device, clay_error_t *err);
  * captured batch calls (a 4 MiB per-device arena; a captured batch of n stripes takes
  * n x 130 x 8 bytes, so about a dozen 300-stripe captures fill it, after which capturing
  * such calls fails with CLAY_ERR_DEVICE) and the pooled workspaces pinned to graphs.
- * Call it once every replay of the graphs captured from this library's calls on `device` has
- * completed (synchronise the replay streams) and the graphs are destroyed.  It does not
- * synchronise the device itself, so it is safe while other threads capture unrelated work;
- * it fails (nothing released) while one of this library's calls is inside a capture at that
- * moment.  No reference counterpart. */
+ * The caller MUST first synchronise every stream that replays those graphs and destroy the
+ * graphs: the released workspaces are handed to the next call at once, with no event to wait
+ * on, so a replay still running would race that call.  It does not synchronise the device
+ * itself (that would invalidate another thread's capture in global mode), so it is safe while
+ * other threads capture unrelated work; it fails (nothing released) while one of this
+ * library's calls runs inside a capture, or while a capture that took a workspace or a table
+ * from this library is still open.  No reference counterpart. */
 int clay_release_captured(int device, clay_error_t *err);
 
 /* Bytes of device memory held by the device's buffer pool (tests / monitoring). */

@@ -48,6 +48,26 @@ def test_codeword_single_erasure_runs_repair(oracle_mod, torch_cuda, cfg, sc, lo
         assert int((outs[(e + 1) % c.n] != 0xA5).sum().item()) == 0
 
 
+@pytest.mark.parametrize("mode", ["grouped", "tile"])
+def test_codeword_route_follows_exec_mode(oracle_mod, torch_cuda, mode):
+    """Under exec modes that do not pick the bit-sliced repair kernels ("grouped", "tile": A/B
+    runs) the codeword entry point runs as clay_decode_device, like clay_repair_device's kernel
+    choice; the bytes are the codeword's either way."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    sc = 65536 + 40
+    chunk = c.sub_chunk_no * sc
+    ref = o.encode_array(np.random.default_rng(5).integers(0, 256, c.k * chunk, dtype=np.uint8))
+    full = torch.from_numpy(ref).cuda()
+    prev = clay_amd.set_exec_mode(mode)
+    try:
+        outs = _decode_dev(torch, c, full, [3], chunk)
+        assert clay_amd.last_exec_path() != "bs-repair-stream", (mode, clay_amd.last_exec_path())
+    finally:
+        clay_amd.set_exec_mode(prev)
+    assert np.array_equal(outs[3].numpy(), ref[3])
+
+
 def test_codeword_other_patterns_as_auto(oracle_mod, torch_cuda):
     """Two erasures, and one erasure at a sub-chunk too small for every CU to get a tile: the
     paths auto takes (local decode), bit-exact."""

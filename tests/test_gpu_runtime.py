@@ -492,3 +492,68 @@ def _decode_graph_capture(oracle_mod, torch_cuda, path, er, er2):
     del g, g2
     torch.cuda.synchronize()
     clay_amd.release_captured(0)
+
+
+def test_release_captured_refused_while_capture_open(oracle_mod, torch_cuda):
+    """clay_release_captured while another thread holds a capture open that took a pooled
+    workspace (grouped-executor decode): refused, and the workspace stays with the graph (the
+    pool does not hand it out); once the capture ended, the graph replayed, its stream was
+    synchronised and the graph destroyed, the same call succeeds."""
+    torch = torch_cuda
+    prev = clay_amd.set_exec_mode("grouped")
+    try:
+        c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+        sc = 256
+        chunk = c.sub_chunk_no * sc
+        er = [0, 4, 8, 12]
+        st = torch.cuda.Stream()
+        clay_amd.release_captured(0)
+        clay_amd.release_workspace(0)
+        c.reserve_workspace(chunk)
+        ref = _stripe(o, 10, chunk, 91)
+        full = torch.from_numpy(ref).cuda()
+        outs = torch.zeros((14, chunk), dtype=torch.uint8, device="cuda")
+        args = ([None if j in er else full[j] for j in range(14)], er,
+                [outs[j] if j in er else None for j in range(14)])
+        c.decode_device(*args, chunk, 0, st.cuda_stream)  # prepares the plan outside the capture
+        st.synchronize()
+        inside, release_now, done = threading.Event(), threading.Event(), threading.Event()
+        box = {}
+
+        def capturer():
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    c.decode_device(*args, chunk, 0, torch.cuda.current_stream().cuda_stream)
+                    inside.set()
+                    release_now.wait(60)  # the capture stays open until the main thread tried
+                box["g"] = g
+            except BaseException as ex:  # noqa: BLE001
+                box["err"] = ex
+                inside.set()
+            finally:
+                done.set()
+
+        th = threading.Thread(target=capturer)
+        th.start()
+        assert inside.wait(60)
+        refused = None
+        try:
+            clay_amd.release_captured(0)
+        except clay_amd.DeviceError as ex:
+            refused = str(ex)
+        release_now.set()
+        th.join(120)
+        assert done.is_set() and "err" not in box, box.get("err")
+        assert refused is not None and "pooled workspace" in refused, refused
+        outs.fill_(0)
+        torch.cuda.synchronize()
+        box["g"].replay()
+        torch.cuda.synchronize()
+        for e in er:
+            assert np.array_equal(outs[e].cpu().numpy(), ref[e]), e
+        del box["g"]
+        torch.cuda.synchronize()
+        clay_amd.release_captured(0)  # capture closed, replays done, graph destroyed: accepted
+    finally:
+        clay_amd.set_exec_mode(prev)

@@ -167,3 +167,39 @@ def test_local256_any_subchunk(oracle_mod, torch_cuda, cfg, sc):
             else:
                 assert np.all(got[e] == 0xA5), "parity output written though not requested"
     assert n256 > 10
+
+
+@pytest.mark.parametrize("sc", [512, 64 * 37 + 40])
+def test_local256_misaligned_chunk_pointers(oracle_mod, torch_cuda, sc):
+    """sc % 8 == 0 but chunk pointers offset 1-7 bytes from 8-byte alignment (slices of one
+    larger buffer): the ANY instantiation of k_stream_local256 runs (its full-tile DMA and the
+    16-byte stores at odd addresses), full and partial tiles, inputs and outputs misaligned by
+    different amounts; bytes vs the oracle, neighbouring bytes of the outputs untouched
+    (ADVICE r05)."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc + 99)
+    for k, er in enumerate(([0], [5], [12], [0, 4], [3, 13], [0, 1])):
+        chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+        pitch = chunk + 64
+        src = torch.zeros(c.n * pitch + 64, dtype=torch.uint8, device="cuda")
+        dst = torch.full((c.n * pitch + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        ins, ous = [], []
+        for i in range(c.n):
+            a = i * pitch + 1 + (i + k) % 7       # 1..7 bytes past 8-byte alignment
+            b = i * pitch + 1 + (i + 3 * k + 2) % 7
+            src[a:a + chunk].copy_(torch.from_numpy(chunks[i]))
+            ins.append(None if i in er else src[a:a + chunk])
+            ous.append(dst[b:b + chunk] if i in er and i < c.k else None)
+        c.decode_device(ins, er, ous, chunk)
+        torch.cuda.synchronize()
+        assert clay_amd.last_exec_path() == "stream-local256", (er, clay_amd.last_exec_path())
+        ref = np.frombuffer(o.decode({i: chunks[i] for i in range(c.n) if i not in er}, er),
+                            dtype=np.uint8).reshape(c.k, -1)
+        host = dst.cpu().numpy()
+        for i in range(c.n):
+            b = i * pitch + 1 + (i + 3 * k + 2) % 7
+            if i in er and i < c.k:
+                assert np.array_equal(host[b:b + chunk], ref[i]), (sc, er, i)
+                assert host[b - 1] == 0x5A and host[b + chunk] == 0x5A, (sc, er, i)
