@@ -79,24 +79,34 @@ def cur_sw(node, row):
     return ((row >> 1) & 1) * 8
 
 
-# round-6 map: digit 2 of the column (bits 0-1) and bit 5 from the wave, so a wave's lanes share d2
-# (waves 4-7: d2 in {2, 3}, whose section-2 companions are the shortened nodes); in-lane column
-# bits k = c bits 2-4; swizzle from row bit 3 (k bit 1) and the node's bit 1 within its section
-def new_map(w, k):
-    d2 = (w & 1) | (((w >> 2) & 1) << 1)
-    return d2 | (k << 2) | (((w >> 1) & 1) << 5)
+# round-6 maps (stream_encode.hpp StreamEnc::spec): digit 2 of the column (bits 0-1) and bit wb
+# from the wave, so a wave's lanes share d2 (waves 4-7: d2 in {2, 3}, whose section-2 companions
+# are the shortened nodes); in-lane column bits k = c bits (kb0, kb1, kb2); swizzle from row bit
+# swb and the node's bit 1 within its section
+SPECS = {1: (2, 3, 4, 5, 3), 3: (2, 3, 4, 5, 3), 4: (3, 2, 4, 5, 3), 5: (4, 3, 2, 5, 3),
+         6: (5, 4, 3, 2, 5), 7: (2, 5, 4, 3, 5), 8: (4, 5, 3, 2, 5), 9: (4, 5, 3, 2, 5)}
 
 
-def new_sw(node, row):
-    return (((row >> 3) & 1) ^ (((node % 4) >> 1) & 1)) * 8
+def spec_map(kb0, kb1, kb2, wb, swb):
+    def cm(w, k):
+        d2 = (w & 1) | (((w >> 2) & 1) << 1)
+        return d2 | ((k & 1) << kb0) | (((k >> 1) & 1) << kb1) | (((k >> 2) & 1) << kb2) | (((w >> 1) & 1) << wb)
+
+    def sw(node, row):
+        return (((row >> swb) & 1) ^ (((node % 4) >> 1) & 1)) * 8
+    return cm, sw
 
 
 def main():
-    for name, cm, sw in (("round-5 map", cur_map, cur_sw), ("round-6 map", new_map, new_sw)):
+    maps = [("round-5 map", cur_map, cur_sw)] + [(f"round-6 map {m} {v}",) + spec_map(*v) for m, v in SPECS.items()]
+    bad = 0
+    for name, cm, sw in maps:
         cols = sorted(cm(w, k) for w in range(8) for k in range(8))
         assert cols == list(range(64)), name
-        print(name, conflicts(cm, sw))
-    return 0
+        r = conflicts(cm, sw)
+        bad += sum(v[0] for v in r.values())
+        print(name, r)
+    return 1 if bad else 0
 
 
 if __name__ == "__main__":

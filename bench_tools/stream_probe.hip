@@ -193,21 +193,68 @@ int main(int argc, char **argv) {
     }
     if (argc > 2 && argv[2][0] == 'n') {  // round-6 lane map (MAP 1: light section 2 on waves 4-7; MAP 2: on 0-3)
         printf("sc %u lane map A/B, back-to-back (200 launches after 50 untimed)\n", sc);
-        if (argv[2][1] == 't') {  // segment timing of both maps
+        if (argv[2][1] == 't') {  // segment timing of the maps
             timing_report<4096, 0>(a, 200);
-            printf("---- map 1\n");
-            timing_report<4096, 1>(a, 200);
+            printf("---- map 3\n");
+            timing_report<4096, 3>(a, 200);
+            return 0;
+        }
+        // bytes of every map against map 0 (the library's, parity-tested against the oracle)
+        const size_t pbytes = 4 * chunk;
+        std::vector<uint8_t> ref(pbytes), got(pbytes);
+        auto snap = [&](std::vector<uint8_t> &v) {
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpy(v.data(), par, pbytes, hipMemcpyDeviceToHost);
+        };
+        (void)hipMemset(par, 0, pbytes);
+        run_b2b<4, 0, 0>(a, 1, 0);
+        snap(ref);
+        auto check = [&](const char *name) {
+            snap(got);
+            printf("  bytes %s == map 0: %s\n", name, ref == got ? "yes" : "NO");
+            (void)hipMemset(par, 0, pbytes);
+        };
+        run_b2b<4, 0, 1>(a, 1, 0); check("map 1");
+        run_b2b<4, 0, 3>(a, 1, 0); check("map 3");
+        run_b2b<4, 0, 4>(a, 1, 0); check("map 4");
+        run_b2b<4, 0, 5>(a, 1, 0); check("map 5");
+        run_b2b<4, 0, 6>(a, 1, 0); check("map 6");
+        run_b2b<4, 0, 7>(a, 1, 0); check("map 7");
+        run_b2b<4, 0, 8>(a, 1, 0); check("map 8");
+        run_b2b<4, 0, 9>(a, 1, 0); check("map 9");
+        if (argv[2][1] == '8') {  // map 8 / 9 (red skip A/B), map 0, priorities
+            for (int rr = 0; rr < 3; rr++) {
+                rep("b2b full, map 0 (round 5)", run_b2b<4, 0, 0>(a, 200));
+                rep("b2b full, map 8", run_b2b<4, 0, 8>(a, 200));
+                rep("b2b full, map 9 (map 8 without red skip)", run_b2b<4, 0, 9>(a, 200));
+                rep("b2b full, map 8, waves 4-7 prio 1", run_b2b<4, 16, 8>(a, 200));
+                rep("b2b full, map 8, no sched barriers", run_b2b<4, 16384, 8>(a, 200));
+                rep("b2b full, map 8, sched barrier / 2 nodes", run_b2b<4, 32768, 8>(a, 200));
+                rep("b2b memory only, map 8", run_b2b<4, 1, 8>(a, 200));
+                rep("b2b live math only, map 8", run_b2b<4, 262146, 8>(a, 200));
+                rep("b2b live reads + math, map 8", run_b2b<4, 262144, 8>(a, 200));
+                rep("b2b math + stores, map 8", run_b2b<4, 2, 8>(a, 200));
+            }
+            timing_report<4096, 8>(a, 200);
             return 0;
         }
         for (int rr = 0; rr < 3; rr++) {
             rep("b2b full, map 0 (round 5)", run_b2b<4, 0, 0>(a, 200));
-            rep("b2b full, map 1 (light waves 4-7)", run_b2b<4, 0, 1>(a, 200));
-            rep("b2b full, map 2 (light waves 0-3)", run_b2b<4, 0, 2>(a, 200));
-            rep("b2b live math only, map 0", run_b2b<4, 262146, 0>(a, 200));
-            rep("b2b live math only, map 1", run_b2b<4, 262146, 1>(a, 200));
-            rep("b2b math + stores, map 1", run_b2b<4, 2, 1>(a, 200));
+            rep("b2b memory only, map 0", run_b2b<4, 1, 0>(a, 200));
+            rep("b2b full, map 1 (k 2,3,4 pair 16)", run_b2b<4, 0, 1>(a, 200));
             rep("b2b memory only, map 1", run_b2b<4, 1, 1>(a, 200));
-            rep("b2b live reads + math, map 1", run_b2b<4, 262144, 1>(a, 200));
+            rep("b2b full, map 3 (map 1, permlane pair 32)", run_b2b<4, 0, 3>(a, 200));
+            rep("b2b full, map 4 (k 3,2,4 pair 32)", run_b2b<4, 0, 4>(a, 200));
+            rep("b2b memory only, map 4", run_b2b<4, 1, 4>(a, 200));
+            rep("b2b full, map 5 (k 4,3,2 pair 64)", run_b2b<4, 0, 5>(a, 200));
+            rep("b2b memory only, map 5", run_b2b<4, 1, 5>(a, 200));
+            rep("b2b full, map 6 (k 5,4,3 pair 128)", run_b2b<4, 0, 6>(a, 200));
+            rep("b2b memory only, map 6", run_b2b<4, 1, 6>(a, 200));
+            rep("b2b full, map 7 (k 2,5,4 pair 16)", run_b2b<4, 0, 7>(a, 200));
+            rep("b2b memory only, map 7", run_b2b<4, 1, 7>(a, 200));
+            rep("b2b full, map 8 (k 4,5,3 pair 64)", run_b2b<4, 0, 8>(a, 200));
+            rep("b2b memory only, map 8", run_b2b<4, 1, 8>(a, 200));
+            rep("b2b live math only, map 1", run_b2b<4, 262146, 1>(a, 200));
         }
         return 0;
     }

@@ -1392,7 +1392,8 @@ static Error launch_stream(CodeState &cs, const DevProps &prop, const uint8_t *c
         for (int i = 0; i < S::K; i++)
             if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
                 return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
-    Error ae = lds_attr_once(reinterpret_cast<const void *>(&bs::k_stream_encode<KD, LOADERS>), Kn::LDS_BYTES, prop.dev);
+    Error ae = lds_attr_once(reinterpret_cast<const void *>(&bs::k_stream_encode<KD, LOADERS, 0, bs::kStreamEncMap>),
+                             Kn::LDS_BYTES, prop.dev);
     if (ae) return ae;
     // XCD region: sc / 8 rounded up to 32 bytes; one workgroup per CU
     const uint32_t region = uint32_t(((sc + 7) / 8 + 31) / 32 * 32);
@@ -1406,7 +1407,7 @@ static Error launch_stream(CodeState &cs, const DevProps &prop, const uint8_t *c
         a.tiles_per_xcd = region;
         a.nslots = nslots;
         a.ntiles = 0;
-        bs::k_stream_encode<KD, LOADERS><<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
+        bs::k_stream_encode<KD, LOADERS, 0, bs::kStreamEncMap><<<dim3(nslots * 8), dim3(Kn::BLOCK), Kn::LDS_BYTES, stream>>>(a);
         CLAY_HIP(hipGetLastError());
         t_last_launches++;
     }

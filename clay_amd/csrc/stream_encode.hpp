@@ -144,27 +144,53 @@ struct StreamEnc {
     // exactly those pairs, so own and companion reads are bank-conflict free (companions of
     // sections 0/1 keep c mod 4; section 2's companion row is shared = broadcast).
     __host__ __device__ static constexpr uint32_t sw(uint32_t r) { return ((r >> 1) & 1u) * 8u; }
-    // Round-6 map (MAP 1 / 2).  Compute lane (wave w, lane l): part p = l & 7, in-lane column index
-    // k = l >> 3 = column bits 2-4 (digit 1 and the low bit of digit 0), the wave supplies digit 2
-    // (bits 0-1) and bit 5.  Digit 2 per wave makes section 2 wave-uniform: for d2 in {2, 3} the
-    // PRT companions of nodes 8, 9 are the shortened nodes 10, 11 (zero), so U = C for 8 and 9 and
-    // U = 0 for 10 and 11 -- a light section-2 step of two plain node folds (section_light).
-    // MAP 1 puts d2 in {2, 3} on waves 4-7 (the younger wave of each SIMD, the one that loses the
-    // VALU arbitration); MAP 2 on waves 0-3.  The LDS image is swizzled per node and row,
-    // piece k of row r of node (Y, x) at slot k ^ swn(x, r), swn = 8 (bit 3 of r ^ bit 1 of x):
-    // own and companion reads of every section step stay bank-conflict free
-    // (bench_tools/lds_conflicts.py models both maps: 0 extra cycles).  The DPP store pair is
-    // columns c, c ^ 4 (lane bit 3 = column bit 2): rows z and z + 16.
-    static constexpr uint32_t PAIR = MAP == 0 ? 4u : 16u;  // row distance of the DPP store pair
+    // Round-6 maps (MAP >= 1).  Compute lane (wave w, lane l): part p = l & 7, in-lane column index
+    // k = l >> 3 (its three bits are column bits kb0, kb1, kb2 of c), the wave supplies digit 2
+    // (column bits 0-1) and column bit wb.  Digit 2 per wave makes section 2 wave-uniform: for
+    // d2 in {2, 3} the PRT companions of nodes 8, 9 are the shortened nodes 10, 11 (zero), so U = C
+    // for 8 and 9 and U = 0 for 10 and 11 -- a light section-2 step of two plain node folds
+    // (section2_u<2>).  The light waves are 4-7 (the younger wave of each SIMD, the one that loses
+    // the VALU arbitration; MAP 2: waves 0-3).  The LDS image is swizzled per node and row, piece k
+    // of row r of node (Y, x) at slot k ^ swn(x, r), swn = 8 (bit swb of r ^ bit 1 of x): own and
+    // companion reads of every section step stay bank-conflict free for the maps below
+    // (bench_tools/lds_conflicts.py: 0 extra cycles).  The store pair is lane ^ 8 (DPP; columns c,
+    // c ^ 2^kb0: rows z, z + 4 * 2^kb0) or, MAP 3, lane ^ 16 through v_permlane16_swap (c ^ 2^kb1).
+    // The maps differ in which parity rows one store instruction writes (memory-only A/B).
+    // redskip: the heavy waves' section-2 red vertex (x = d2) without companion read and PRT
+    struct MapSpec {
+        int kb0, kb1, kb2, wb, swb;
+        bool light_old, pswap, redskip;
+    };
+    static constexpr MapSpec spec() {
+        switch (MAP) {
+            case 1: return {2, 3, 4, 5, 3, false, false, true};
+            case 2: return {2, 3, 4, 5, 3, true, false, true};
+            case 3: return {2, 3, 4, 5, 3, false, true, true};
+            case 4: return {3, 2, 4, 5, 3, false, false, true};
+            case 5: return {4, 3, 2, 5, 3, false, false, true};
+            case 6: return {5, 4, 3, 2, 5, false, false, true};
+            case 7: return {2, 5, 4, 3, 5, false, false, true};
+            case 8: return {4, 5, 3, 2, 5, false, false, true};
+            case 9: return {4, 5, 3, 2, 5, false, false, false};
+            default: return {0, 1, 2, 3, 1, false, false, false};  // MAP 0: unused
+        }
+    }
+    static constexpr MapSpec MS = spec();
+    static constexpr bool PSWAP = MS.pswap;
+    static constexpr uint32_t PAIR = MAP == 0 ? 4u : (4u << (PSWAP ? MS.kb1 : MS.kb0));  // row distance of the store pair
     __device__ static int colmap(int w, int k) {
         if constexpr (MAP == 0) return 8 * w + k;
-        const int hi = MAP == 1 ? ((w >> 2) & 1) : (((w >> 2) & 1) ^ 1);
-        return (w & 1) | (hi << 1) | (k << 2) | (((w >> 1) & 1) << 5);
+        const int hi = MS.light_old ? (((w >> 2) & 1) ^ 1) : ((w >> 2) & 1);
+        return (w & 1) | (hi << 1) | ((k & 1) << MS.kb0) | (((k >> 1) & 1) << MS.kb1) | (((k >> 2) & 1) << MS.kb2) |
+               (((w >> 1) & 1) << MS.wb);
     }
-    __device__ static bool light_wave(int w) { return MAP == 1 ? w >= 4 : (MAP == 2 ? w < 4 : false); }
     __host__ __device__ static constexpr uint32_t swn(uint32_t x, uint32_t r) {
-        return MAP == 0 ? sw(r) : ((((r >> 3) & 1u) ^ ((x >> 1) & 1u))) * 8u;
+        return MAP == 0 ? sw(r) : ((((r >> MS.swb) & 1u) ^ ((x >> 1) & 1u))) * 8u;
     }
+    // does the swizzle's row bit lie in digit y (then a companion row's bit comes from x)?
+    static constexpr bool sw_in_digit(int y) { return MS.swb == dshift(y) || MS.swb == dshift(y) + 1; }
+    // piece-pair swap of the companion read of node x in section y (the x part of its swizzle)
+    static constexpr int comp_swap(int y, int x) { return sw_in_digit(y) ? ((x >> (MS.swb - dshift(y))) & 1) : 0; }
 
     // ---------------- loader ----------------
     struct Loader {
@@ -269,7 +295,7 @@ struct StreamEnc {
         if constexpr (MAP != 0) {
             // own: row c, slot p ^ swn(x, c); the node's bit-1 term swaps the two pieces (load_x)
             const uint32_t uc = uint32_t(c), up = uint32_t(part);
-            L.own[0] = uc * 256u + ((up ^ (((uc >> 3) & 1u) * 8u)) * 16u);
+            L.own[0] = uc * 256u + ((up ^ (((uc >> MS.swb) & 1u) * 8u)) * 16u);
             L.own[1] = L.own[0] ^ 128u;
 #pragma unroll
             for (int y = 0; y < 3; y++) {
@@ -277,9 +303,9 @@ struct StreamEnc {
                 L.cy[y] = (c >> sh) & 3;
                 const uint32_t cy = uint32_t(L.cy[y]);
                 const uint32_t row0 = (uc & ~(3u << sh)) * 256u + cy * uint32_t(NODE_BYTES);
-                // companion row c' = c[y := x]: bit 3 of c' is c's for y = 0, 2 and x's for y = 1
-                // (the x term then swaps the pieces, load_x)
-                const uint32_t rb = y == 1 ? 0u : ((uc >> 3) & 1u);
+                // companion row c' = c[y := x]: its swizzle bit is c's unless that bit lies in digit
+                // y, then x's (the x term swaps the pieces, load_x)
+                const uint32_t rb = sw_in_digit(y) ? 0u : ((uc >> MS.swb) & 1u);
                 L.cb[y][0] = row0 + ((up ^ ((rb ^ ((cy >> 1) & 1u)) * 8u)) * 16u);
                 L.cb[y][1] = L.cb[y][0] ^ 128u;
             }
@@ -318,9 +344,10 @@ struct StreamEnc {
 #pragma unroll
                 for (int w = 0; w < 8; w++) o[w] = 0;
             }
-            if ((Y * Q + L.cy[Y]) < KD) {
+            // (section 2: digit 2 is wave-uniform, so the red vertex's companion read is skipped)
+            if ((Y * Q + L.cy[Y]) < KD && (Y != 2 || !MS.redskip || X != L.cy[Y])) {
                 constexpr uint32_t step = uint32_t(256) << dshift(Y);
-                constexpr int hb = Y == 1 ? bx : 0;
+                constexpr int hb = comp_swap(Y, X);
                 read32(slot + L.cb[Y][hb] + X * step, slot + L.cb[Y][hb ^ 1] + X * step, cv);
             } else {
 #pragma unroll
@@ -352,6 +379,13 @@ struct StreamEnc {
     template <int Y, int X>
     __device__ static void prt_x(const uint32_t (&o)[8], const uint32_t (&cv)[8], const LaneS &L, uint32_t (&u)[8]) {
         const int cy = L.cy[Y];
+        if constexpr (MAP != 0 && Y == 2 && MS.redskip) {
+            if (X == cy) {  // wave-uniform red vertex: U = C, no PRT
+#pragma unroll
+                for (int w = 0; w < 8; w++) u[w] = o[w];
+                return;
+            }
+        }
         const bool creal = (Y * Q + cy) < KD;
         const uint32_t keep = (creal && X != cy) ? 0xffffffffu : 0u;
         const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
@@ -381,23 +415,48 @@ struct StreamEnc {
         });
     }
 
-    // Section 2 on a light wave (MAP 1 / 2, digit 2 of every lane's column in {2, 3}): the
-    // companions of nodes 8 and 9 are shortened (zero), so U = C (transforms.rs:42-55 with C* = 0)
-    // and the shortened nodes' U are zero (no fold); no companion reads, no PRT.
-    template <int SBN = 1>
-    __device__ __forceinline__ static void section_light(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
+    // Section 2 with a wave-uniform digit 2 (MAP >= 1): D2 = the wave's d2 (2 stands for 2 and 3).
+    // Node x of the section: own value real iff 8 + x < KD; PRT companion (node (2, D2) at layer
+    // z[2 := x], transforms.rs:42-55) real iff x != D2 (else the red vertex: U = C) and 8 + D2 < KD.
+    // So for KD = 10: D2 in {2, 3} (the light waves) U = C for nodes 8, 9 and U = 0 for 10, 11 (no
+    // fold); D2 in {0, 1}: the red node without companion read or PRT, the shortened nodes U = gamma
+    // C*.  Everything is compile-time: no masks, no per-lane branches.
+    template <int D2, int SBN = 1>
+    __device__ __forceinline__ static void section2_u(const uint8_t *slot, const LaneS &L, uint32_t (&acc)[Q * 8]) {
         static_assert(MAP != 0, "wave-uniform digit 2");
+        constexpr int Y = 2;
+        auto load = [&](auto xc, uint32_t (&o)[8], uint32_t (&cv)[8]) BS_INL {
+            constexpr int x = decltype(xc)::value;
+            constexpr bool own_real = Y * Q + x < KD;
+            constexpr bool comp_real = x != D2 && Y * Q + D2 < KD;
+            constexpr int bx = (x >> 1) & 1;
+            if constexpr (own_real) read32(slot + x * NODE_BYTES + L.own[bx], slot + x * NODE_BYTES + L.own[bx ^ 1], o);
+            constexpr int hb = comp_swap(Y, x);
+            if constexpr (comp_real) read32(slot + L.cb[Y][hb] + x * 256, slot + L.cb[Y][hb ^ 1] + x * 256, cv);
+        };
+        uint32_t o[2][8], cv[2][8];
+        load(std::integral_constant<int, 0>{}, o[0], cv[0]);
         sfor<Q>([&](auto xc) BS_INL {
             constexpr int x = decltype(xc)::value;
-            if constexpr (2 * Q + x < KD) {
-                constexpr int bx = (x >> 1) & 1;
+            constexpr bool own_real = Y * Q + x < KD;
+            constexpr bool comp_real = x != D2 && Y * Q + D2 < KD;
+            if constexpr (x + 1 < Q) load(std::integral_constant<int, x + 1>{}, o[(x + 1) & 1], cv[(x + 1) & 1]);
+            if constexpr (own_real || comp_real) {
                 uint32_t u[8];
-                read32(slot + x * NODE_BYTES + L.own[bx], slot + x * NODE_BYTES + L.own[bx ^ 1], u);
-                if constexpr (CSE) K6::template fold_x_cse<2, x>(u, acc);
-                else K6::template fold_x<2, x>(u, acc);
+#pragma unroll
+                for (int w = 0; w < 8; w++) {
+                    if constexpr (own_real && comp_real) u[w] = xor_xtime4_masked(o[x & 1][w], cv[x & 1][w], 0xfefefefeu, 0x1d1d1d1du);
+                    else if constexpr (comp_real) u[w] = xor_xtime4_masked(0u, cv[x & 1][w], 0xfefefefeu, 0x1d1d1d1du);
+                    else u[w] = o[x & 1][w];
+                }
+                if constexpr (CSE) K6::template fold_x_cse<Y, x>(u, acc);
+                else K6::template fold_x<Y, x>(u, acc);
                 if constexpr (SBN > 0) __builtin_amdgcn_sched_barrier(0);
             }
         });
+        // a distinct marker ends every copy: otherwise SimplifyCFG sinks the copies' common tail
+        // (the last fold) below the switch and the accumulators meet in phis (spilled)
+        asm volatile("; section2_u end %0" ::"n"(D2));
     }
 
     // ---------------- compute: outputs ----------------
@@ -405,20 +464,35 @@ struct StreamEnc {
     // pieces p and 8 + p of its row; lanes c and c ^ 1 (lane ^ 8, same row of 16 lanes) swap
     // halves by DPP so that each 16-byte store instruction of a wave writes 4 whole
     // 256-byte row runs (even columns, then odd columns) instead of 8 rows x 128 B.
+    // The store pair's halves: lanes of a column and of its partner (lane ^ 8 in the same DPP row,
+    // or MAP 3: lane ^ 16, the other row of a row pair) exchange halves so that lo holds the even
+    // column's row (the even lane piece p, the odd lane piece 8 + p) and hi the odd column's.
+    __device__ __forceinline__ static void pair_halves(const uint32_t (&cv)[8], uint32_t (&lo)[4], uint32_t (&hi)[4]) {
+        if constexpr (PSWAP) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const auto r = __builtin_amdgcn_permlane16_swap(cv[i], cv[4 + i], false, false);
+                lo[i] = r[0];
+                hi[i] = r[1];
+            }
+        } else {
+            const bool odd = (threadIdx.x >> 3) & 1u;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t send = odd ? cv[i] : cv[4 + i];
+                const uint32_t r = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, false));  // row_ror:8
+                lo[i] = odd ? r : cv[i];      // row of the even column, piece (odd ? 8 : 0) + p
+                hi[i] = odd ? cv[4 + i] : r;  // row of the odd column
+            }
+        }
+    }
     template <int X>
     __device__ __forceinline__ static void put(const BsArgs &a, uint32_t (&cv)[8], uint32_t z, StreamTile t, uint32_t prel,
                                bool ragged, uint32_t &sink) {
         transpose8(cv);
         if (SINK && !ragged) {
-            const bool odd = (threadIdx.x >> 3) & 1u;
-            uint32_t r[4], lo[4], hi[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t send = odd ? cv[i] : cv[4 + i];
-                r[i] = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, false));
-                lo[i] = odd ? r[i] : cv[i];
-                hi[i] = odd ? cv[4 + i] : r[i];
-            }
+            uint32_t lo[4], hi[4];
+            pair_halves(cv, lo, hi);
             sink ^= xor3(xor3(lo[0], lo[1], lo[2]), xor3(lo[3], hi[0], hi[1]), hi[2] ^ hi[3]);
             sink += X;  // keeps the per-output order visible (no cancellation across outputs)
             return;
@@ -429,15 +503,9 @@ struct StreamEnc {
         }
         (void)sink;
         if (!ragged) {
-            const bool odd = (threadIdx.x >> 3) & 1u;
-            uint32_t r[4], lo[4], hi[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t send = odd ? cv[i] : cv[4 + i];
-                r[i] = uint32_t(__builtin_amdgcn_update_dpp(0, int(send), 0x128, 0xf, 0xf, false));  // row_ror:8
-                lo[i] = odd ? r[i] : cv[i];      // row of the even column, piece (odd ? 8 : 0) + p
-                hi[i] = odd ? cv[4 + i] : r[i];  // row of the odd column
-            }
+            const bool odd = PSWAP ? ((threadIdx.x >> 4) & 1u) : ((threadIdx.x >> 3) & 1u);
+            uint32_t lo[4], hi[4];
+            pair_halves(cv, lo, hi);
             uint32_t off = (z - (odd ? PAIR : 0u)) * uint32_t(a.sc);
             asm volatile("" : "+v"(off));  // keep the 16 (node, layer) offsets out of LICM
             off += t.b0 + prel + (odd ? 128u : 0u);
@@ -585,6 +653,11 @@ struct TimeAcc {
     }
 };
 
+// The lane map the library launches (round 6: map 8, light section-2 waves 4-7; same-box A/B on
+// the BASELINE stripe, profiles/r06/encode/: 0.3311-0.3317 ms vs 0.3349-0.3355 for map 0 and
+// 0.3484-0.3489 for the round-5 kernel)
+constexpr int kStreamEncMap = 8;
+
 template <int KD, int LOADERS, int PROBE = 0, int MAP = 0>
 __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_encode(BsArgs a) {
     using Kn = StreamEnc<KD, LOADERS, (PROBE >> 6) & 3, (PROBE >> 8) & 3, ((PROBE >> 10) & 1) == 0, (PROBE & 262144) != 0,
@@ -663,7 +736,8 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
     const int c = Kn::colmap(wave, (int(threadIdx.x) >> 3) & 7), part = int(threadIdx.x) & 7;
-    const bool light = Kn::light_wave(wave);
+    // PROBE 1048576 (probe builds): section 2 of the heavy waves as compile-time copies per d2 too
+    constexpr bool SEC2U = (PROBE & 1048576) != 0;
     const uint32_t prel = uint32_t(part) * 16u;
     uint32_t acc[Kn::Q * 8];
     typename K6::Hold H;
@@ -685,10 +759,14 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
     StreamTile pt{0, 0};
     auto end_any = [&](int ge, StreamTile t) BS_INL {
         const bool ragged = t.vend < t.b0 + uint32_t(Kn::W);
-        if (ge == 0) Kn::template end_group<0>(a, acc, H, c, t, prel, ragged, sink);
-        else if (ge == 1) Kn::template end_group<1>(a, acc, H, c, t, prel, ragged, sink);
-        else if (ge == 2) Kn::template end_group<2>(a, acc, H, c, t, prel, ragged, sink);
-        else Kn::template end_group<3>(a, acc, H, c, t, prel, ragged, sink);
+        // opaque per-call copy of the column: the store rows derived from it are computed here,
+        // not hoisted out of the tile loop into long-lived (spilled) registers
+        int cc = c;
+        asm volatile("" : "+v"(cc));
+        if (ge == 0) Kn::template end_group<0>(a, acc, H, cc, t, prel, ragged, sink);
+        else if (ge == 1) Kn::template end_group<1>(a, acc, H, cc, t, prel, ragged, sink);
+        else if (ge == 2) Kn::template end_group<2>(a, acc, H, cc, t, prel, ragged, sink);
+        else Kn::template end_group<3>(a, acc, H, cc, t, prel, ragged, sink);
     };
     TimeAcc T;
     T.t_start = TM ? __builtin_amdgcn_s_memtime() : 0;
@@ -750,8 +828,18 @@ __global__ __launch_bounds__((StreamEnc<KD, LOADERS>::BLOCK)) void k_stream_enco
             constexpr bool BAL = (PROBE & 131072) != 0;
             if (y == 0) Kn::template section<0, SBN, BAL>(smem, L, acc);
             else if (y == 1) Kn::template section<1, SBN, BAL>(smem + Kn::REGION, L, acc);
-            else if (MAP != 0 && light) {
-                if constexpr (MAP != 0) Kn::template section_light<SBN>(smem + 2 * Kn::REGION, L, acc);
+            else if constexpr (MAP != 0) {
+                // wave-uniform digit 2 (an SGPR): compile-time section-2 copies
+                const int d2 = L.cy[2];
+                if constexpr (SEC2U) {
+                    if (d2 == 0) Kn::template section2_u<0, SBN>(smem + 2 * Kn::REGION, L, acc);
+                    else if (d2 == 1) Kn::template section2_u<1, SBN>(smem + 2 * Kn::REGION, L, acc);
+                    else Kn::template section2_u<2, SBN>(smem + 2 * Kn::REGION, L, acc);
+                } else {
+                    // light waves (d2 in {2, 3}): the compile-time copy; d2 in {0, 1}: the generic step
+                    if (d2 >= 2) Kn::template section2_u<2, SBN>(smem + 2 * Kn::REGION, L, acc);
+                    else Kn::template section<2, SBN, BAL>(smem + 2 * Kn::REGION, L, acc);
+                }
             } else Kn::template section<2, SBN, BAL>(smem + 2 * Kn::REGION, L, acc);
         }
         if constexpr (TM) T.add(1, y, t0);
