@@ -38,7 +38,22 @@ struct DecArgs {
     // 5 / 6 = none erased, all alive and only node 0 / nodes 0-1 used (k_stream_local256 only),
     // -1 = the run-time copy
     int32_t scase[4];
+    // k_stream_fused2 with two erasures in a section (round 6): per erased row r, pinfo[r] = bit 0:
+    // r has a partner (the other erased node of its section), bits 1-2 the partner's row, 3-4 the
+    // section, 5-6 r's digit, 7-8 the partner's digit (packed: few scalar registers); npair = rows
+    // with a partner (both-erased PFT pairs, transforms.rs:108-125, inverted after the rounds)
+    uint32_t pinfo[4];
+    uint32_t npair;
+    // k_stream_fused2: bit y = section y's loads do not all fit the ring during step y - 1 (two
+    // neighbouring sections with more alive nodes than the ring holds): the rest is issued after
+    // B_y and waited for behind a second barrier
+    uint32_t split;
 };
+// k_stream_fused2: solver work items per lane and round (passes of 64 lanes over targets x 8
+// pieces, per iscore level); the host declines patterns whose target counts exceed them
+constexpr int kF2Iters[4] = {9, 8, 2, 1};
+constexpr int kF2Off[4] = {0, 9, 17, 19};
+constexpr int kF2Items = 20;
 // local decode: v_perm table of det^-1 = (1 + gamma^2)^-1 (pair inversion, transforms.rs:108-125)
 constexpr int kDecDetInv = 80;
 // 3 KiB: k_stream_local copies them into LDS with three 1 KiB LDS-DMA instructions

@@ -1982,8 +1982,35 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
 
 hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
 
-// Fused decode v2 (stream_fused2.hpp): one erasure in each y-section, one launch, rounds of tile k-1
-// on the loader waves while tile k streams.  Ring of 10 - ne node buffers + the S/C region.
+// Rounds of k_stream_fused2 (stream_fused2.hpp): per section Y with an erasure and iscore level L,
+// the targets are the layers z with z_Y in E_Y and exactly L - 1 other sections y with z_y in E_y;
+// the kernel holds kF2Iters[L - 1] passes of 64 lanes x (8-byte piece) per level.
+static bool f2_fits(const uint32_t (&emask)[4]) {
+    for (int Y = 0; Y < 4; Y++) {
+        if (!emask[Y]) continue;
+        for (int L = 1; L <= 4; L++) {
+            uint32_t n = 0;
+            for (uint32_t z = 0; z < 256; z++) {
+                int red = 0;
+                bool ty = false;
+                for (int y = 0; y < 4; y++) {
+                    const uint32_t d = (z >> (2 * (3 - y))) & 3u;
+                    const bool in = (emask[y] >> d) & 1u;
+                    red += in ? 1 : 0;
+                    if (y == Y) ty = in;
+                }
+                n += (ty && red == L) ? 1u : 0u;
+            }
+            if ((n * 8u + 63u) / 64u > uint32_t(bs::kF2Iters[L - 1])) return false;
+        }
+    }
+    return true;
+}
+
+// Fused decode v2 (stream_fused2.hpp): erasures in at least two y-sections with at most two per
+// section (round 6: two in a section -- both-erased PFT pairs inverted after the rounds), one launch,
+// rounds of tile k-1 on the loader waves while tile k streams.  Ring of 10 - ne node buffers + the
+// S/C region.
 template <int KD>
 static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uint8_t *const *cin, uint8_t *const *cout,
                                   const std::vector<uint8_t> &erased, size_t sc, hipStream_t stream, bool *done) {
@@ -1991,16 +2018,32 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     bs::DecArgs a;
     std::vector<uint32_t> tabs;
     bool ok = false;
-    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 1, a, tabs, &ok);
+    Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 2, a, tabs, &ok);
     if (e || !ok) return e;
-    if (a.ne < 2) return Error{};  // 2-4 erasures in distinct sections (the rounds' target enumeration)
+    if (a.ne < 2) return Error{};
+    if (!f2_fits(a.emask)) return Error{};  // more round targets than the kernel's item registers
+    // both-erased pairs: per erased row, the other erased row of its section
+    a.npair = 0;
+    for (int r = 0; r < 4; r++) a.pinfo[r] = 0;
+    for (int y = 0; y < 4; y++) {
+        if (__builtin_popcount(a.emask[y]) != 2) continue;
+        const uint32_t x1 = uint32_t(__builtin_ctz(a.emask[y])), x2 = 31u - uint32_t(__builtin_clz(a.emask[y]));
+        const int r1 = a.rix[4 * y + int(x1)], r2 = a.rix[4 * y + int(x2)];
+        a.pinfo[r1] = 1u | uint32_t(r2) << 1 | uint32_t(y) << 3 | x1 << 5 | x2 << 7;
+        a.pinfo[r2] = 1u | uint32_t(r1) << 1 | uint32_t(y) << 3 | x2 << 5 | x1 << 7;
+        a.npair += 2;
+    }
+    if (a.npair) perm_table(gamma_det_inv(), &tabs[bs::kDecDetInv * 8]);  // (1 + gamma^2)^-1
     const uint32_t RB = 10 - a.ne;  // the S/C region takes ne of the 10 node buffers of LDS
-    // the loads of a step are issued during the step before it (the ring holds both), also
-    // across tiles: section 3 of tile k and section 0 of tile k + 1
+    // the loads of a step are issued during the step before it when the ring holds both; else
+    // (round 6: two neighbouring sections with 7-8 alive nodes and RB = 6) the step is split: the
+    // rest of its loads after its barrier, behind a second one.  Section 0 of tile k + 1 needs no
+    // split: every ring buffer is free at B_r(k), before its barrier.
+    a.split = 0;
     for (int y = 0; y < 4; y++) {
         const uint32_t ny = a.sec_off[y + 1] - a.sec_off[y];
-        const uint32_t nn = y < 3 ? a.sec_off[y + 2] - a.sec_off[y + 1] : a.sec_off[1] - a.sec_off[0];
-        if (ny > RB || ny + nn > RB) return Error{};
+        if (ny > RB) return Error{};
+        if (y > 0 && (a.sec_off[y] - a.sec_off[y - 1]) + ny > RB) a.split |= 1u << y;
     }
     a.ring = RB;
     const uint32_t per_xcd = uint32_t(std::max(1, prop.cus / 8));

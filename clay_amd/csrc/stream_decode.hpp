@@ -135,7 +135,7 @@ struct StreamDec {
     };
     struct Map {
         uint32_t x0, x1, n;
-        __device__ Map(uint32_t sc, uint32_t region, uint32_t ns, uint32_t xcd, uint32_t slot) {
+        __device__ __forceinline__ Map(uint32_t sc, uint32_t region, uint32_t ns, uint32_t xcd, uint32_t slot) {
             x0 = xcd * region;
             x1 = x0 + region < sc ? x0 + region : sc;
             n = 0;
@@ -144,7 +144,7 @@ struct StreamDec {
                 n = nt > slot ? (nt - slot + ns - 1) / ns : 0;
             }
         }
-        __device__ Tile tile(uint32_t k, uint32_t slot, uint32_t ns) const {
+        __device__ __forceinline__ Tile tile(uint32_t k, uint32_t slot, uint32_t ns) const {
             const uint32_t b0 = x0 + (slot + k * ns) * uint32_t(W);
             return {b0, b0 + uint32_t(W) < x1 ? b0 + uint32_t(W) : x1};
         }
@@ -219,6 +219,10 @@ struct StreamDec {
             } else {
                 lds_barrier();  // step (k, Y) landed (the loaders waited before this barrier)
             }
+            // k_stream_fused2 split step (the ring held only part of this section's loads during
+            // the step before): the loaders issue the rest after the barrier above, wait, and join
+            // this second one
+            if ((a.split >> Y) & 1u) lds_barrier();
             if constexpr ((PROBE & 2) != 0) return;
             if constexpr (!RT && (PROBE & 128) == 0) {
                 switch (a.scase[Y]) {
@@ -313,9 +317,10 @@ struct StreamDec {
                     for (int w = 0; w < 8; w++) o[X][w] = 0;
                 }
             });
-            if constexpr (RT) {
+            if (RT || (!CT && __builtin_popcount(emY) > 1)) {
                 // every erased node (G, A): Out((G, A), slot g) = gamma * C((G, g), slot A), 0 at
-                // slot A and where (G, g) has no data (erased: a both-erased pair, inverted later)
+                // slot A and where (G, g) has no data (erased: a both-erased pair, inverted later;
+                // k_stream_local, and k_stream_fused2's run-time copy for two erasures in G)
                 sfor<4>([&](auto ac) BS_INL {
                     constexpr int A = decltype(ac)::value;
                     if (!((emY >> A) & 1u)) return;

@@ -178,6 +178,17 @@ if __name__ == "__main__":
             ("local", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1])),
             ("local", lambda: decode_cfg(9, 4, 12, 1 << 30, [0])),
             ("local", lambda: decode_cfg(9, 4, 12, 1 << 30, [0, 4])),
+            # round 6: 4-erasure patterns with two erasures in one section ((2,1,1) and (2,2)
+            # sections: 750 of the 1,001 4-erasure patterns), k_stream_fused2 in auto, and the
+            # grouped executor they ran on before; {0,8,9,10} runs a split step (neighbouring
+            # sections beyond the ring)
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4, 8])),
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4, 12])),
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4, 5])),
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [8, 9, 0, 4])),
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 8, 9, 10])),
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4, 8], "grouped")),
+            ("two", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 1, 4, 5], "grouped")),
             # clay_decode_device_codeword: one erasure rebuilt by the repair kernel from whole
             # chunks (charged the repair route's bytes)
             ("codeword", lambda: decode_cfg(10, 4, 13, 1 << 30, [0], codeword=True)),

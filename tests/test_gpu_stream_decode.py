@@ -54,7 +54,7 @@ def stream_path(c, er):
         for e in er:
             per[_internal(c, e) // c.q] += 1
         return "stream-local256" if max(per) == 1 or [n for n in per if n] == [2] else "stream-local"
-    if fused2_eligible(c, er):
+    if fused2_eligible(c, er, two=True):
         return "stream-fused2"
     return None
 
@@ -149,16 +149,45 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, stream_m
         assert np.array_equal(a[e], b[e]), e
 
 
-def fused2_eligible(c, er):
-    """k_stream_fused2: 2-4 erasures in distinct y-sections and a ring of 10 - e node buffers that
-    holds any two neighbouring sections' surviving real nodes."""
-    if not stream_eligible(c, er) or not 2 <= len(er) <= c.t:
+def f2_fits(c, er):
+    """The host's round-capacity check (engine.hip f2_fits): per section Y with an erasure and
+    iscore level L, the layers with z_Y in E_Y and L erased sections red, <= kF2Iters[L - 1]
+    passes of 64 lanes x 8-byte pieces."""
+    iters = [9, 8, 2, 1]
+    em = [0] * c.t
+    for e in er:
+        i = _internal(c, e)
+        em[i // c.q] |= 1 << (i % c.q)
+    for Y in range(c.t):
+        if not em[Y]:
+            continue
+        for L in range(1, 5):
+            n = 0
+            for z in range(256):
+                d = [(z >> (2 * (3 - y))) & 3 for y in range(4)]
+                red = sum(1 for y in range(4) if (em[y] >> d[y]) & 1)
+                n += 1 if (em[Y] >> d[Y]) & 1 and red == L else 0
+            if (n * 8 + 63) // 64 > iters[L - 1]:
+                return False
+    return True
+
+
+def fused2_eligible(c, er, two=False):
+    """k_stream_fused2: 2-4 erasures in distinct y-sections (two=True: at most two per section,
+    round 6) whose round targets fit the kernel's item registers, and a ring of 10 - e node buffers
+    that holds any two neighbouring sections' surviving real nodes."""
+    per = [0] * c.t
+    for e in er:
+        per[_internal(c, e) // c.q] += 1
+    if not 2 <= len(er) <= c.t or max(per) > (2 if two else 1) or not f2_fits(c, er):
         return False
     alive = [0] * c.t
     for i in range(c.n):
         if i not in er:
             alive[_internal(c, i) // c.q] += 1
     rb = 10 - len(er)
+    if two:  # round 6: neighbouring sections beyond the ring run as split steps
+        return max(alive) <= rb
     return all(alive[y] + alive[(y + 1) % c.t] <= rb for y in range(c.t))  # incl. section 3 -> next tile's 0
 
 
@@ -219,3 +248,67 @@ def test_fused2_decode_codeword_incl_parity_and_grouped(oracle_mod, torch_cuda, 
                 assert np.array_equal(a[e], b[e]), (er, e)
     finally:
         clay_amd.set_exec_mode(prev)
+
+
+def _two_in_a_section(c, r=4):
+    """The 4-erasure patterns with two erasures in a section and the others elsewhere ((2,1,1) and
+    (2,2) sections), which round 6 moved from the grouped executor to k_stream_fused2."""
+    out = []
+    for er in itertools.combinations(range(c.n), r):
+        per = [0] * c.t
+        for e in er:
+            per[_internal(c, e) // c.q] += 1
+        if max(per) == 2 and not local_eligible(c, list(er)) and fused2_eligible(c, list(er), two=True):
+            out.append(list(er))
+    return out
+
+
+@pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
+@pytest.mark.parametrize("sc", [512, 520, 64 * 37 + 40])
+def test_fused2_two_erasures_in_a_section_random_inputs(oracle_mod, torch_cuda, cfg, sc):
+    """Auto mode on 4-erasure patterns with two erasures in one y-section ((2,1,1): {0,1,4,8},
+    {8,9,0,4}; (2,2): {0,1,4,5}; with parity nodes: {0,1,4,12}) and a random sample of the rest:
+    k_stream_fused2 runs (the both-erased PFT pairs inverted after the rounds), erased data chunks
+    bit-exact vs the oracle on random (non-codeword) chunks, ragged and sc % 16 == 8 tiles."""
+    torch = torch_cuda
+    c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc * 7 + cfg[0])
+    allp = _two_in_a_section(c)
+    assert len(allp) == (750 if cfg == (10, 4, 13) else 540)
+    pats = [p for p in ([0, 1, 4, 8], [8, 9, 0, 4], [0, 1, 4, 5], [0, 1, 4, 12], [4, 5, 12, 13], [0, 8, 9, 10])
+            if sorted(p) in allp]
+    pats += [allp[i] for i in rng.permutation(len(allp))[:14]]
+    for er in pats:
+        chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+        got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
+        assert clay_amd.last_exec_path() == "stream-fused2", (er, clay_amd.last_exec_path())
+        ref = _oracle_erased(o, c, chunks, er)
+        for e in er:
+            if e < c.k:
+                assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e)
+
+
+@pytest.mark.parametrize("sc", [520, 64 * 8 * 33 + 24])
+def test_fused2_two_erasures_in_a_section_codeword_and_grouped(oracle_mod, torch_cuda, sc):
+    """(2,1,1) / (2,2) patterns incl. parity nodes on a codeword (every rebuilt chunk, parity
+    included, equals the encoded one) and on random chunks against the grouped plan executor
+    (parity outputs included)."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    chunk = c.sub_chunk_no * sc
+    ref = o.encode_array(np.random.default_rng(sc).integers(0, 256, c.k * chunk, dtype=np.uint8))
+    for er in ([0, 1, 4, 12], [12, 13, 0, 4], [12, 13, 1, 2], [8, 9, 12, 13], [2, 3, 6, 13]):
+        got = _decode_dev(torch, c, ref, er, chunk)
+        assert clay_amd.last_exec_path() == "stream-fused2", er
+        for e in er:
+            assert np.array_equal(got[e], ref[e]), (er, e)
+        chunks = np.random.default_rng(sc + er[0]).integers(0, 256, (c.n, chunk), dtype=np.uint8)
+        a = _decode_dev(torch, c, chunks, er, chunk)
+        prev = clay_amd.set_exec_mode("grouped")
+        try:
+            b = _decode_dev(torch, c, chunks, er, chunk)
+        finally:
+            clay_amd.set_exec_mode(prev)
+        for e in er:
+            assert np.array_equal(a[e], b[e]), (er, e)
