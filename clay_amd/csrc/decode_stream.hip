@@ -56,7 +56,7 @@ hipError_t launch_stream_local_kernel(int kd, int g, const bs::DecArgs &a, hipSt
     return hipErrorInvalidValue;
 }
 
-template <int KD, int PROBE = 0>
+template <int KD, int PROBE = 0, bool TWO = false>
 static hipError_t launch_f2(const bs::DecArgs &a, hipStream_t stream, int dev) {
     static std::mutex mu;
     static std::set<int> done;
@@ -64,18 +64,24 @@ static hipError_t launch_f2(const bs::DecArgs &a, hipStream_t stream, int dev) {
     {
         std::lock_guard<std::mutex> lk(mu);
         if (!done.count(dev)) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_fused2<KD, 3, PROBE>),
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bs::k_stream_fused2<KD, 3, PROBE, TWO>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             done.insert(dev);
         }
     }
-    bs::k_stream_fused2<KD, 3, PROBE><<<dim3(a.nslots * 8), dim3(bs::StreamDec<KD, 3>::BLOCK), lds, stream>>>(a);
+    bs::k_stream_fused2<KD, 3, PROBE, TWO><<<dim3(a.nslots * 8), dim3(bs::StreamDec<KD, 3>::BLOCK), lds, stream>>>(a);
     return hipGetLastError();
 }
 
-// the fused decode v2 (stream_fused2.hpp): one erasure per y-section
-hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev) {
+// the fused decode v2 (stream_fused2.hpp): erasures in distinct y-sections, or (two = true, round
+// 6) two erasures in some section
+hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev, bool two) {
+    if (two) {
+        if (kd == 10) return launch_f2<10, 0, true>(a, stream, dev);
+        if (kd == 9) return launch_f2<9, 0, true>(a, stream, dev);
+        return hipErrorInvalidValue;
+    }
 #ifdef CLAY_DECODE_PROBES
     const int probe = tuning().decode_probe;
     // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only, 36 no rounds / presolve,

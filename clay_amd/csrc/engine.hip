@@ -1980,7 +1980,8 @@ static Error launch_stream_local(CodeState &cs, const DevProps &prop, const uint
     return Error{};
 }
 
-hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev);  // decode_stream.hip
+hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev,
+                                       bool two);  // decode_stream.hip
 
 // Rounds of k_stream_fused2 (stream_fused2.hpp): per section Y with an erasure and iscore level L,
 // the targets are the layers z with z_Y in E_Y and exactly L - 1 other sections y with z_y in E_y;
@@ -2050,7 +2051,10 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
     e = dec_tables(cs, prop, tabs, stream, &a.tabs);
     if (e) return e;
-    CLAY_HIP(launch_stream_fused2_kernel(KD, a, stream, prop.dev));
+    bool two = false;
+    for (int y = 0; y < 4; y++) two = two || __builtin_popcount(a.emask[y]) > 1;
+    if (!two) a.split = 0;  // (no pattern with one erasure per section overflows the ring)
+    CLAY_HIP(launch_stream_fused2_kernel(KD, a, stream, prop.dev, two));
     t_last_launches += 1;
     t_last_exec = "stream-fused2";
     *done = true;

@@ -207,7 +207,7 @@ struct StreamDec {
     // straight-line PRT + fold code without the per-node branches, which the scheduler interleaves
     // across nodes; -1 (an ignored node in the section: fewer than 4 erasures) takes the run-time
     // copy.  PROBE 128 (probe library): always the run-time copy.
-    template <int PROBE, bool RT = false, bool SB = true>
+    template <int PROBE, bool RT = false, bool SB = true, bool MULTI = false>
     __device__ __forceinline__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
                                    uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {
         sfor<4>([&](auto yc) BS_INL {
@@ -226,15 +226,15 @@ struct StreamDec {
             if constexpr ((PROBE & 2) != 0) return;
             if constexpr (!RT && (PROBE & 128) == 0) {
                 switch (a.scase[Y]) {
-                case 0: section<Y, 0, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 1: section<Y, 1, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 2: section<Y, 2, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 3: section<Y, 3, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 4: section<Y, 4, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                default: section<Y, -1, false, SB>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 0: section<Y, 0, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 1: section<Y, 1, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 2: section<Y, 2, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 3: section<Y, 3, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 4: section<Y, 4, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                default: section<Y, -1, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
                 }
             } else {
-                section<Y, -1, RT, SB>(a, smem, qbase, c0, poff0, xeG, S, R);
+                section<Y, -1, RT, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R);
             }
         });
     }
@@ -249,7 +249,8 @@ struct StreamDec {
 
     // one step of phase A.  XE >= 0: the compile-time structure of scase XE (node (Y, XE) erased,
     // XE = 4: none; every other node used); XE = -1: the pattern's masks at run time
-    template <int Y, int XE, bool RT, bool SB>
+    // MULTI (k_stream_fused2<.., TWO>): the run-time copy also takes two erasures in section G
+    template <int Y, int XE, bool RT, bool SB, bool MULTI = false>
     __device__ __forceinline__ static void section(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0,
                                    int xeG, uint32_t (&S)[32], uint32_t R) {
         constexpr bool CT = XE >= 0;
@@ -317,7 +318,7 @@ struct StreamDec {
                     for (int w = 0; w < 8; w++) o[X][w] = 0;
                 }
             });
-            if (RT || (!CT && __builtin_popcount(emY) > 1)) {
+            if (RT || (MULTI && !CT && __builtin_popcount(emY) > 1)) {
                 // every erased node (G, A): Out((G, A), slot g) = gamma * C((G, g), slot A), 0 at
                 // slot A and where (G, g) has no data (erased: a both-erased pair, inverted later;
                 // k_stream_local, and k_stream_fused2's run-time copy for two erasures in G)

@@ -37,33 +37,31 @@ namespace bs {
 // for 4 / 3 / 2 erasures (4 / 5 / 6 passes), level 2 27 / 24 / 16 (4 / 3 / 2), level 3 9 / 4
 // (2 / 1), level 4 1 (1).  Four erasures with two in a section (round 6: (2,1,1) and (2,2)
 // sections): level 1 72 / 64 targets (9 / 8 passes), level 2 48 / 64 (6 / 8), level 3 8 (1)
-// (bench_tools/f2_targets.py counts them).
+// (tests/test_gpu_stream_decode.py::f2_fits and engine.hip f2_fits count them).
 // (kF2Iters / kF2Off / kF2Items: decode_args.hpp, shared with the host's eligibility check)
 template <int N>
 using IC = std::integral_constant<int, N>;
 
-// S/C region layout (round 6): layer z's 64-byte row of an erased row's 16 KiB block at
-// rz(z) = 64 * ((z & ~3) | q(z)), q(z) = XOR of z's four base-4 digits -- a permutation of the
-// four rows of each aligned group.  The compute lanes' layers 4 c0 + g and the rounds' target
-// layers (digits of one section fixed, the others enumerated) then spread over the four 64-byte
-// quarters of a 256-byte bank row (bench_tools/lds_conflicts_fused2.py: 0 extra cycles on the
-// compute side, 60 % fewer in the rounds; the plain layout z * 64 put 4 columns on one quarter:
-// SQ_LDS_BANK_CONFLICT 13.5 M per decode).
-#ifndef CLAY_F2_SWZ
-#define CLAY_F2_SWZ 1
-#endif
-// CLAY_F2_SWZ=0 (A/B builds): the plain layout, row of layer z at 64 z
-constexpr bool kF2Swz = CLAY_F2_SWZ != 0;
-__host__ __device__ constexpr uint32_t f2_qz(uint32_t z) { return kF2Swz ? (z ^ (z >> 2) ^ (z >> 4) ^ (z >> 6)) & 3u : z & 3u; }
-__host__ __device__ constexpr uint32_t f2_rz(uint32_t z) { return ((z & ~3u) | f2_qz(z)) * 64u; }
+// S/C region layout: row of layer z of an erased row's 16 KiB block at 64 z.  (Round 6 measured a
+// swizzled layout -- quarter = XOR of the layer's base-4 digits, bench_tools/lds_conflicts_fused2.py:
+// SQ_LDS_BANK_CONFLICT 13.5 M -> 3.2 M per decode -- at 0.58 vs 0.51 ms for {0,4,8,12}: the extra
+// address arithmetic in the loader waves' rounds, which bound the kernel, costs more than the
+// conflicts; profiles/r06/decode/.)
 
 // PROBE (bench_tools only; the library instantiates 0): 1 = loader waves skip the rounds,
 // 2 = no output stores, 4 = no phase-A math, 8 = no presolve, 16 = s_memtime segment timing
 // (workgroup 0 prints the totals of compute wave 0 and loader wave 0), 64 = rounds at priority 0,
 // 128 = phase A without the per-section compile-time copies (StreamDec::phase_a)
-template <int KD, int G, int PROBE = 0>
+// TWO: the instantiation for two erasures in a section (both-erased pairs, split steps, the larger
+// round item sets); patterns with at most one erasure per section run TWO = false, whose hot code
+// is the round-5 kernel's (the larger TWO kernel ran {0,4,8,12} 15 % slower: 0.58 vs 0.51 ms)
+template <int KD, int G, int PROBE = 0, bool TWO = false>
 __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(DecArgs a) {
     using Kn = StreamDec<KD, G>;
+    // round work items per lane and level: kF2Iters (TWO) or the round-5 {6, 4, 2, 1}
+    static constexpr int IT[4] = {TWO ? kF2Iters[0] : 6, TWO ? kF2Iters[1] : 4, TWO ? kF2Iters[2] : 2, TWO ? kF2Iters[3] : 1};
+    static constexpr int OFF[4] = {0, IT[0], IT[0] + IT[1], IT[0] + IT[1] + IT[2]};
+    static constexpr int NIT = IT[0] + IT[1] + IT[2] + IT[3];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t xcd = blockIdx.x & 7u, wslot = blockIdx.x >> 3, ns = a.nslots;
@@ -98,6 +96,102 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         // three X != x_e(Y), loaded once into registers (tile-invariant; zero for an X outside the
         // used shards: no dropped term, decode.rs:374)
         const uint32_t ne = a.ne;
+        // the round tables (tg), the lane's work items (rb) and the section's erased digits:
+        // the round-5 enumeration for one erasure per section (!TWO), the general one for up to two
+        GfTab tg[3][4];
+        uint32_t rb[NIT];
+        uint32_t Y = uint32_t(li), x1 = 0, x2 = 0, nY = 0, Xj[3] = {0, 0, 0};
+        uint32_t src1 = 0, src2 = 0, wy64 = 0;
+        auto setup_one = [&]() BS_INL {
+        uint32_t xe[4], esec = 0;
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            xe[y] = a.emask[y] ? uint32_t(__builtin_ctz(a.emask[y])) : 0u;
+            esec |= (a.emask[y] ? 1u : 0u) << y;
+        }
+        const uint32_t xY = xe[Y];
+        const bool wact = (esec >> Y) & 1u;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
+            const bool use = wact && ((a.used >> (4u * Y + X)) & 1u);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                // loaded unconditionally (every table exists), then masked: zero = no term
+                const uint32_t keep = (use && uint32_t(r) < ne) ? ~0u : 0u;
+                const GfTab t = load_tab_c(tabc + (16u + (4u * Y + X) * 4u + uint32_t(r)) * 8u);
+                tg[j][r] = GfTab{t.w0 & keep, t.w1 & keep, t.w2 & keep, t.w3 & keep, t.w4 & keep};
+                asm volatile("" : "+v"(tg[j][r].w0), "+v"(tg[j][r].w1), "+v"(tg[j][r].w2), "+v"(tg[j][r].w3),
+                             "+v"(tg[j][r].w4));
+            }
+        }
+        // C(e_Y, .): rix read unconditionally (xY = 0 for a section without an erasure), then the
+        // value selected -- a select between loads would become a load through a selected pointer
+        // and move the kernel arguments to scratch memory
+        const uint32_t rY = opq(uint32_t(a.rix[4u * Y + xY]));
+        const uint8_t *src5 = scr + (wact ? rY : 0u) * BUF;
+        wy64 = Kn::wt(int(Y)) * 64u;
+        // the lane's work items of every round, tile-invariant: byte offset (layer without section
+        // Y's digit) x 64 + 8-byte piece, ~0 = none.  Level L's targets: z_Y = x_e(Y), L - 1 of the
+        // other erased sections red (subset `sub`), base-3 digits for the other erased sections,
+        // base-4 digits for the sections without an erasure; the lowest-weight section's digit
+        // varies fastest (neighbouring items on different LDS banks)
+        const uint32_t no = uint32_t(__builtin_popcount(esec)) - (wact ? 1u : 0u);  // other erased sections
+        const uint32_t n4 = 4u - uint32_t(__builtin_popcount(esec));                // sections without one
+        sfor<4>([&](auto yc) BS_INL {
+            constexpr int y = decltype(yc)::value;
+            constexpr uint32_t L = uint32_t(y) + 1u;
+            uint32_t c3 = 1, c4 = 1, nsub = 0;
+            for (uint32_t i = 0; i + (L - 1u) < no; i++) c3 *= 3u;
+            for (uint32_t i = 0; i < n4; i++) c4 *= 4u;
+            for (uint32_t m = 0; m < (1u << no); m++) nsub += uint32_t(__builtin_popcount(m)) == L - 1u ? 1u : 0u;
+            const uint32_t per = c3 * c4, total = (wact && L - 1u <= no) ? nsub * per : 0u;
+#pragma unroll
+            for (int i = 0; i < IT[y]; i++) {
+                const uint32_t it = uint32_t(lane) + 64u * uint32_t(i);
+                const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
+                if (ci >= total) {
+                    rb[OFF[y] + i] = ~0u;
+                    continue;
+                }
+                const uint32_t sub = ci / per;
+                uint32_t v = ci % per, mask = 0, cnt = 0;
+                for (uint32_t m = 0; m < (1u << no); m++)
+                    if (uint32_t(__builtin_popcount(m)) == L - 1u) {
+                        if (cnt == sub) mask = m;
+                        cnt++;
+                    }
+                uint32_t zb = 0, o = 0;  // o: index among the other erased sections (descending)
+                sfor<4>([&](auto qc) BS_INL {
+                    constexpr int yy = 3 - decltype(qc)::value;
+                    if (uint32_t(yy) == Y) return;
+                    const uint32_t xy = xe[yy];
+                    uint32_t dgt;
+                    if ((esec >> yy) & 1u) {
+                        if ((mask >> o) & 1u) {
+                            dgt = xy;
+                        } else {
+                            const uint32_t u = v % 3u;
+                            v /= 3u;
+                            dgt = u + (u >= xy ? 1u : 0u);
+                        }
+                        o++;
+                    } else {
+                        dgt = v & 3u;
+                        v >>= 2;
+                    }
+                    zb += dgt * Kn::wt(yy);
+                });
+                rb[OFF[y] + i] = zb * 64u + d8;
+            }
+        });
+            x1 = x2 = xY;
+            nY = 1;
+            src1 = src2 = uint32_t(src5 - scr);
+#pragma unroll
+            for (int j = 0; j < 3; j++) Xj[j] = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
+        };
+        auto setup_two = [&]() BS_INL {
         // erased nodes per section: em[y] (one or two bits: round 6 takes two in a section)
         uint32_t em[4], esec = 0;
 #pragma unroll
@@ -105,12 +199,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             em[y] = a.emask[y];
             esec |= (em[y] ? 1u : 0u) << y;
         }
-        const uint32_t Y = uint32_t(li), emY = em[Y];
+        const uint32_t emY = em[Y];
         const bool wact = (esec >> Y) & 1u;
         // the section's erased digits x1 <= x2 (x2 = x1 for one erasure) and its used digits X_j:
         // the three (one erasure) or two (two erasures) X outside E_Y
-        const uint32_t x1 = emY ? uint32_t(__builtin_ctz(emY)) : 0u, x2 = emY ? 31u - uint32_t(__builtin_clz(emY)) : 0u;
-        uint32_t Xj[3];
+        x1 = emY ? uint32_t(__builtin_ctz(emY)) : 0u, x2 = emY ? 31u - uint32_t(__builtin_clz(emY)) : 0u;
         {
             uint32_t pool = ~emY & 15u;
 #pragma unroll
@@ -119,7 +212,6 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 pool &= pool - 1u;
             }
         }
-        GfTab tg[3][4];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const uint32_t X = Xj[j] & 3u;
@@ -138,20 +230,16 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         // an erasure), then the values selected -- a select between loads would become a load
         // through a selected pointer and move the kernel arguments to scratch memory
         const uint32_t r1 = opq(uint32_t(a.rix[4u * Y + x1])), r2 = opq(uint32_t(a.rix[4u * Y + x2]));
-        const uint32_t src1 = (wact ? r1 : 0u) * BUF, src2 = (wact ? r2 : 0u) * BUF;
-        // layer step of section Y's digit in the region (f2_rz): through the quarter for Y = 3
-        const uint32_t wy64 = Y == 3u ? 0u : Kn::wt(int(Y)) * 64u;
-        // quarter of the layer zb + X * wt(Y): swizzled q(zb) ^ X; plain X for Y = 3, else zb's low digit
-        const uint32_t qmask = kF2Swz || Y == 3u ? ~0u : 0u;
+        src1 = (wact ? r1 : 0u) * BUF, src2 = (wact ? r2 : 0u) * BUF;
+        wy64 = Kn::wt(int(Y)) * 64u;
         // the lane's work items of every round, tile-invariant: (target layer without section Y's
-        // digit & ~3) x 64 + 8-byte piece, bit 2 = the target's red erased node of section Y is x2,
-        // bits 0-1 = the XOR of the layer's other digits (f2_rz); ~0 = none.  Level L's targets:
+        // digit) x 64 + 8-byte piece, bit 0 = the target's red erased node of section Y is x2 (else
+        // x1); ~0 = none.  Level L's targets:
         // z_Y in E_Y, L - 1 of the other erased sections red (subset `sub`: z_y in E_y), the other
         // erased sections non-red (z_y outside E_y), free digits for the sections without an
         // erasure; the lowest-weight section's digit varies fastest (neighbouring items on
         // different LDS banks), the choice of z_Y slowest
-        uint32_t rb[kF2Items];
-        const uint32_t nY = uint32_t(__builtin_popcount(emY));
+        nY = uint32_t(__builtin_popcount(emY));
         sfor<4>([&](auto yc) BS_INL {
             constexpr int y = decltype(yc)::value;
             constexpr uint32_t L = uint32_t(y) + 1u;
@@ -177,12 +265,12 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     if (!(m & ~others) && uint32_t(__builtin_popcount(m)) == L - 1u) total += per_sub(m);
             total *= nY;
 #pragma unroll
-            for (int i = 0; i < kF2Iters[y]; i++) {
+            for (int i = 0; i < IT[y]; i++) {
                 const uint32_t it = uint32_t(lane) + 64u * uint32_t(i);
                 uint32_t ci = it >> 3;
                 const uint32_t d8 = (it & 7u) * 8u;
                 if (ci >= total) {
-                    rb[kF2Off[y] + i] = ~0u;
+                    rb[OFF[y] + i] = ~0u;
                     continue;
                 }
                 const uint32_t tsel = ci / (total / nY);  // 0: z_Y = x1, 1: z_Y = x2
@@ -217,30 +305,34 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     }
                     zb += dgt * Kn::wt(yy);
                 });
-                rb[kF2Off[y] + i] = (zb & ~3u) * 64u + d8 + (tsel << 2) + f2_qz(zb);
+                rb[OFF[y] + i] = zb * 64u + d8 + tsel;
             }
         });
+        };
+        if constexpr (!TWO) {
+            setup_one();
+        } else {
+            setup_two();
+        }
         // ---- the round of iscore level LV + 1 of tile k - 1 (passes [I0, I1) of the lane's items):
         // every target layer z of the level red in section Y adds sum over X != x_e(Y) of
         // A_(Y,X) C(e_Y, z[Y := X]) (the three terms summed in registers, one 64-bit LDS atomic per
         // row)
-        auto round = [&](auto lvc, auto i0c, auto i1c) BS_INL {
-            constexpr int LV = decltype(lvc)::value, I0 = decltype(i0c)::value, I1 = decltype(i1c)::value;
+        auto round = [&](auto lvc) BS_INL {
+            constexpr int LV = decltype(lvc)::value;
 #pragma unroll
-            for (int i = I0; i < I1; i++) {
-                // opaque per round: the item's addresses are computed here, not hoisted out of the
-                // tile loop (4 addresses x 20 items of long-lived registers)
-                const uint32_t ob = opq(rb[kF2Off[LV] + i]);
+            for (int i = 0; i < IT[LV]; i++) {
+                const uint32_t ob = rb[OFF[LV] + i];
                 if (ob == ~0u) continue;
-                const uint32_t obb = ob & ~7u, oq = ob & 3u;
-                const bool t2 = (ob >> 2) & 1u;  // the target's red erased node: x2 (else x1)
+                const uint32_t obb = TWO ? ob & ~7u : ob;
+                const bool t2 = TWO && (ob & 1u);  // the target's red erased node: x2 (else x1)
                 const uint8_t *src = scr + (t2 ? src2 : src1);
                 uint32_t acc[4][2] = {};
 #pragma unroll
                 for (int j = 0; j < 3; j++) {
-                    if (j == 2 && nY == 2u) break;  // two erasures in the section: two used X
+                    if (TWO && j == 2 && nY == 2u) break;  // two erasures in the section: two used X
                     const uint32_t X = Xj[j];
-                    const uint2 cv = *reinterpret_cast<const uint2 *>(src + obb + X * wy64 + ((oq ^ (X & qmask)) << 6));
+                    const uint2 cv = *reinterpret_cast<const uint2 *>(src + obb + X * wy64);
                     const GfIdx i0 = gf_idx(cv.x), i1 = gf_idx(cv.y);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
@@ -249,7 +341,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     }
                 }
                 const uint32_t xt = t2 ? x2 : x1;
-                const uint32_t oz = obb + xt * wy64 + ((oq ^ (xt & qmask)) << 6);
+                const uint32_t oz = obb + xt * wy64;
 #pragma unroll
                 for (int r = 0; r < 4; r++)
                     if (uint32_t(r) < ne)  // the region holds ne rows
@@ -282,14 +374,14 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                     t0 = t1;
                 }
                 if (k < ntile) issue_upto(k * NT + a.sec_off[y] + RB);
-                if ((a.split >> y) & 1u) {  // the rest of step (k, y)'s loads, then a second barrier
+                if (TWO && ((a.split >> y) & 1u)) {  // the rest of step (k, y)'s loads, then a second barrier
                     if (k < ntile) wait_vm_rt(int((issued - (k * NT + a.sec_off[y + 1])) * uint32_t(Kn::BPL)));
                     lds_barrier();
                 }
                 if (k == 0 || (PROBE & 1)) return;
                 // PROBE 64: the round at the compute waves' priority (the DMA issue above stays at 3)
                 if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(0);
-                round(IC<y>{}, IC<0>{}, IC<kF2Iters[y]>{});
+                round(IC<y>{});
                 if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(3);
                 if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
             });
@@ -298,7 +390,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             // the compute waves are past phase A(k): every ring buffer is free, so the next tile's
             // first RB loads stream during the presolve, the region hand-over and the stores
             if (k + 1u < ntile) issue_upto((k + 1u) * NT + RB);
-            if (a.npair) lds_barrier();  // B_p(k): the compute lanes read C(k-1) and the pair partners
+            if (TWO && a.npair) lds_barrier();  // B_p(k): the compute lanes read C(k-1) and the pair partners
             if constexpr (TM) tm_end += __builtin_amdgcn_s_memtime() - t0;
         }
         wait_vm0();
@@ -328,7 +420,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
-            Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false>(a, smem, k * NT, c0, poff0, xeG, S,
+            Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false, TWO>(a, smem, k * NT, c0, poff0, xeG, S,
                                                                                     RB, TM ? &tm_pabar : nullptr);
             // bit planes -> bytes
 #pragma unroll
@@ -344,7 +436,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
 #pragma unroll
             for (int y = 0; y < 4; y++) {  // B_y(ntile): the last tile's rounds (+ the split steps' second barriers)
                 lds_barrier();
-                if ((a.split >> y) & 1u) lds_barrier();
+                if (TWO && ((a.split >> y) & 1u)) lds_barrier();
             }
         }
         if constexpr (TM) {
@@ -410,18 +502,18 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         uint2 ov[16];  // [row r][slot g]
         {
             const uint32_t z0 = Kn::layer0(opq(c0));
-            if (!a.npair) {
+            if (!TWO || !a.npair) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     if (uint32_t(r) >= a.ne) continue;
 #pragma unroll
                     for (int g = 0; g < 4; g++) {
-                        uint2 *q = reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + f2_rz(z0 + uint32_t(g) * Kn::wt(G)) + 8u * p);
+                        uint2 *q = reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p);
                         if (k >= 1) ov[r * 4 + g] = *q;
                         if (k < ntile) *q = make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
                     }
                 }
-            } else {
+            } else if constexpr (TWO) {
                 if (k >= 1) {
                     const GfTab dinv = load_tab_c(tabc + kDecDetInv * 8);
 #pragma unroll
@@ -434,11 +526,11 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
 #pragma unroll
                         for (int g = 0; g < 4; g++) {
                             const uint32_t z = z0 + uint32_t(g) * Kn::wt(G);
-                            ov[r * 4 + g] = *reinterpret_cast<const uint2 *>(scr + uint32_t(r) * BUF + f2_rz(z) + 8u * p);
+                            ov[r * 4 + g] = *reinterpret_cast<const uint2 *>(scr + uint32_t(r) * BUF + z * 64u + 8u * p);
                             if (haspr && ((z >> sh) & 3u) == xo) {
                                 const uint32_t zp = (z & ~(3u << sh)) | (xr << sh);
                                 const uint2 u2 =
-                                    *reinterpret_cast<const uint2 *>(scr + pr * BUF + f2_rz(zp) + 8u * p);
+                                    *reinterpret_cast<const uint2 *>(scr + pr * BUF + zp * 64u + 8u * p);
                                 const uint2 u1 = ov[r * 4 + g];
                                 ov[r * 4 + g] =
                                     make_uint2(gf_mul(u1.x ^ gf_xt(u2.x), dinv), gf_mul(u1.y ^ gf_xt(u2.y), dinv));
@@ -453,7 +545,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                         if (uint32_t(r) >= a.ne) continue;
 #pragma unroll
                         for (int g = 0; g < 4; g++)
-                            *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + f2_rz(z0 + uint32_t(g) * Kn::wt(G)) + 8u * p) =
+                            *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p) =
                                 make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
                     }
                 }
