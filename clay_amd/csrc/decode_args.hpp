@@ -48,12 +48,15 @@ struct DecArgs {
     // neighbouring sections with more alive nodes than the ring holds): the rest is issued after
     // B_y and waited for behind a second barrier
     uint32_t split;
+    // k_stream_fused2: byte li = loader wave li's share of the rounds (engine.hip f2_plan): bits
+    // 0-1 its section, 2-3 its part, 4-5 the section's wave count - 1, bit 6 set (0: no rounds)
+    uint32_t lwave;
 };
 // k_stream_fused2: solver work items per lane and round (passes of 64 lanes over targets x 8
-// pieces, per iscore level); the host declines patterns whose target counts exceed them
-constexpr int kF2Iters[4] = {9, 8, 2, 1};
-constexpr int kF2Off[4] = {0, 9, 17, 19};
-constexpr int kF2Items = 20;
+// pieces, per iscore level) of the TWO instantiation (two erasures in a section) and of the other;
+// the host declines patterns whose target counts exceed them (engine.hip f2_plan)
+constexpr int kF2Iters[4] = {5, 4, 2, 1};
+constexpr int kF2Iters1[4] = {6, 4, 2, 1};
 // local decode: v_perm table of det^-1 = (1 + gamma^2)^-1 (pair inversion, transforms.rs:108-125)
 constexpr int kDecDetInv = 80;
 // 3 KiB: k_stream_local copies them into LDS with three 1 KiB LDS-DMA instructions

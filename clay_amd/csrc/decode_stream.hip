@@ -77,13 +77,26 @@ static hipError_t launch_f2(const bs::DecArgs &a, hipStream_t stream, int dev) {
 // the fused decode v2 (stream_fused2.hpp): erasures in distinct y-sections, or (two = true, round
 // 6) two erasures in some section
 hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t stream, int dev, bool two) {
+#ifdef CLAY_DECODE_PROBES
+    const int probe = tuning().decode_probe;
+    // the TWO instantiation: 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only, 40 timing
+    if (two && kd == 10) {
+        switch (probe) {
+        case 31: return launch_f2<10, 1, true>(a, stream, dev);
+        case 32: return launch_f2<10, 2, true>(a, stream, dev);
+        case 34: return launch_f2<10, 4, true>(a, stream, dev);
+        case 35: return launch_f2<10, 13, true>(a, stream, dev);
+        case 40: return launch_f2<10, 16, true>(a, stream, dev);
+        default: break;
+        }
+    }
+#endif
     if (two) {
         if (kd == 10) return launch_f2<10, 0, true>(a, stream, dev);
         if (kd == 9) return launch_f2<9, 0, true>(a, stream, dev);
         return hipErrorInvalidValue;
     }
 #ifdef CLAY_DECODE_PROBES
-    const int probe = tuning().decode_probe;
     // 31 no rounds, 32 no stores, 34 no phase-A math, 35 memory only, 36 no rounds / presolve,
     // 37 no rounds / stores, 38 no rounds / phase-A math (presolve kept), 39 no presolve
     // 40: the full kernel with s_memtime segment timing (workgroup 0 prints its compute wave 0 and

@@ -1984,27 +1984,58 @@ hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t
                                        bool two);  // decode_stream.hip
 
 // Rounds of k_stream_fused2 (stream_fused2.hpp): per section Y with an erasure and iscore level L,
-// the targets are the layers z with z_Y in E_Y and exactly L - 1 other sections y with z_y in E_y;
-// the kernel holds kF2Iters[L - 1] passes of 64 lanes x (8-byte piece) per level.
-static bool f2_fits(const uint32_t (&emask)[4]) {
+// the targets are the layers z with z_Y in E_Y and exactly L - 1 other sections y with z_y in E_y,
+// P(Y, L) = ceil(targets x 8 / 64) passes of 64 lanes x (8-byte piece).  The four loader waves share
+// them: each section with an erasure gets one wave, the spare waves go one by one to the section
+// with the most passes per wave (ties: the lower section), and a section's nw waves take every
+// nw-th pass.  f2_plan packs, per loader wave li, byte li of a.lwave: bits 0-1 its section, 2-3 its
+// part, 4-5 nw - 1, bit 6 set (no section: 0); false when a wave would hold more than the kernel's
+// kF2Iters (TWO) / kF2Iters1 passes of some level.
+static uint32_t f2_targets(const uint32_t (&emask)[4], int Y, int L) {
+    uint32_t n = 0;
+    for (uint32_t z = 0; z < 256; z++) {
+        int red = 0;
+        bool ty = false;
+        for (int y = 0; y < 4; y++) {
+            const uint32_t d = (z >> (2 * (3 - y))) & 3u;
+            const bool in = (emask[y] >> d) & 1u;
+            red += in ? 1 : 0;
+            if (y == Y) ty = in;
+        }
+        n += (ty && red == L) ? 1u : 0u;
+    }
+    return n;
+}
+static bool f2_plan(const uint32_t (&emask)[4], bool two, uint32_t *lwave) {
+    uint32_t P[4][4] = {}, tot[4] = {}, nw[4] = {};
+    int nact = 0;
     for (int Y = 0; Y < 4; Y++) {
         if (!emask[Y]) continue;
+        nact++;
+        nw[Y] = 1;
         for (int L = 1; L <= 4; L++) {
-            uint32_t n = 0;
-            for (uint32_t z = 0; z < 256; z++) {
-                int red = 0;
-                bool ty = false;
-                for (int y = 0; y < 4; y++) {
-                    const uint32_t d = (z >> (2 * (3 - y))) & 3u;
-                    const bool in = (emask[y] >> d) & 1u;
-                    red += in ? 1 : 0;
-                    if (y == Y) ty = in;
-                }
-                n += (ty && red == L) ? 1u : 0u;
-            }
-            if ((n * 8u + 63u) / 64u > uint32_t(bs::kF2Iters[L - 1])) return false;
+            P[Y][L - 1] = (f2_targets(emask, Y, L) * 8u + 63u) / 64u;
+            tot[Y] += P[Y][L - 1];
         }
     }
+    for (int s = nact; s < 4; s++) {
+        int best = -1;
+        for (int Y = 0; Y < 4; Y++)  // tot[Y] / nw[Y] > tot[best] / nw[best]
+            if (nw[Y] && (best < 0 || tot[Y] * nw[best] > tot[best] * nw[Y])) best = Y;
+        if (best < 0) break;
+        nw[best]++;
+    }
+    const int *cap = two ? bs::kF2Iters : bs::kF2Iters1;
+    uint32_t pack = 0;
+    int li = 0;
+    for (int Y = 0; Y < 4; Y++) {
+        for (uint32_t part = 0; part < nw[Y]; part++, li++)
+            pack |= (uint32_t(Y) | part << 2 | (nw[Y] - 1u) << 4 | 64u) << (8 * li);
+        for (int L = 0; L < 4 && nw[Y]; L++)
+            if ((P[Y][L] + nw[Y] - 1u) / nw[Y] > uint32_t(cap[L])) return false;
+        if (two && P[Y][3]) return false;  // the TWO kernel inverts the pairs during the level-4 round's slot
+    }
+    *lwave = pack;
     return true;
 }
 
@@ -2022,7 +2053,9 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     Error e = dec_setup<KD>(cs, cin, cout, erased, sc, 2, a, tabs, &ok);
     if (e || !ok) return e;
     if (a.ne < 2) return Error{};
-    if (!f2_fits(a.emask)) return Error{};  // more round targets than the kernel's item registers
+    bool two = false;
+    for (int y = 0; y < 4; y++) two = two || __builtin_popcount(a.emask[y]) > 1;
+    if (!f2_plan(a.emask, two, &a.lwave)) return Error{};  // more round targets than the kernel's item registers
     // both-erased pairs: per erased row, the other erased row of its section
     a.npair = 0;
     for (int r = 0; r < 4; r++) a.pinfo[r] = 0;
@@ -2051,8 +2084,6 @@ static Error launch_stream_fused2(CodeState &cs, const DevProps &prop, const uin
     a.nslots = std::min(per_xcd, std::max(1u, a.region / 64u));
     e = dec_tables(cs, prop, tabs, stream, &a.tabs);
     if (e) return e;
-    bool two = false;
-    for (int y = 0; y < 4; y++) two = two || __builtin_popcount(a.emask[y]) > 1;
     if (!two) a.split = 0;  // (no pattern with one erasure per section overflows the ring)
     CLAY_HIP(launch_stream_fused2_kernel(KD, a, stream, prop.dev, two));
     t_last_launches += 1;

@@ -58,8 +58,9 @@ using IC = std::integral_constant<int, N>;
 template <int KD, int G, int PROBE = 0, bool TWO = false>
 __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(DecArgs a) {
     using Kn = StreamDec<KD, G>;
-    // round work items per lane and level: kF2Iters (TWO) or the round-5 {6, 4, 2, 1}
-    static constexpr int IT[4] = {TWO ? kF2Iters[0] : 6, TWO ? kF2Iters[1] : 4, TWO ? kF2Iters[2] : 2, TWO ? kF2Iters[3] : 1};
+    // round work items per lane and level (decode_args.hpp)
+    static constexpr int IT[4] = {TWO ? kF2Iters[0] : kF2Iters1[0], TWO ? kF2Iters[1] : kF2Iters1[1],
+                                  TWO ? kF2Iters[2] : kF2Iters1[2], TWO ? kF2Iters[3] : kF2Iters1[3]};
     static constexpr int OFF[4] = {0, IT[0], IT[0] + IT[1], IT[0] + IT[1] + IT[2]};
     static constexpr int NIT = IT[0] + IT[1] + IT[2] + IT[3];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -91,16 +92,20 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         };
         issue_upto(RB);
-        // the rounds' work of this wave: the targets red in section Y = li (one wave per section
-        // with an erasure; the wave of a section without one only loads); the A_(Y,X) tables of its
-        // three X != x_e(Y), loaded once into registers (tile-invariant; zero for an X outside the
-        // used shards: no dropped term, decode.rs:374)
+        // the rounds' work of this wave (a.lwave, engine.hip f2_plan): every nw-th pass, from pass
+        // `part`, over the targets red in section Y (one to four waves per section with an erasure;
+        // a wave without a section only loads); the A_(Y,X) tables of its X outside E_Y, loaded
+        // once into registers (tile-invariant; zero for an X outside the used shards: no dropped
+        // term, decode.rs:374)
         const uint32_t ne = a.ne;
+        const uint32_t lw = (a.lwave >> (8 * li)) & 0xffu;
+        const bool lact = (lw >> 6) & 1u;
+        const uint32_t part = (lw >> 2) & 3u, nw = ((lw >> 4) & 3u) + 1u;
         // the round tables (tg), the lane's work items (rb) and the section's erased digits:
         // the round-5 enumeration for one erasure per section (!TWO), the general one for up to two
         GfTab tg[3][4];
         uint32_t rb[NIT];
-        uint32_t Y = uint32_t(li), x1 = 0, x2 = 0, nY = 0, Xj[3] = {0, 0, 0};
+        uint32_t Y = lw & 3u, x1 = 0, x2 = 0, nY = 0, Xj[3] = {0, 0, 0};
         uint32_t src1 = 0, src2 = 0, wy64 = 0;
         auto setup_one = [&]() BS_INL {
         uint32_t xe[4], esec = 0;
@@ -110,7 +115,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             esec |= (a.emask[y] ? 1u : 0u) << y;
         }
         const uint32_t xY = xe[Y];
-        const bool wact = (esec >> Y) & 1u;
+        const bool wact = lact && ((esec >> Y) & 1u);
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const uint32_t X = uint32_t(j) + (uint32_t(j) >= xY ? 1u : 0u);
@@ -148,7 +153,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t per = c3 * c4, total = (wact && L - 1u <= no) ? nsub * per : 0u;
 #pragma unroll
             for (int i = 0; i < IT[y]; i++) {
-                const uint32_t it = uint32_t(lane) + 64u * uint32_t(i);
+                const uint32_t it = uint32_t(lane) + 64u * (uint32_t(i) * nw + part);
                 const uint32_t ci = it >> 3, d8 = (it & 7u) * 8u;
                 if (ci >= total) {
                     rb[OFF[y] + i] = ~0u;
@@ -200,7 +205,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             esec |= (em[y] ? 1u : 0u) << y;
         }
         const uint32_t emY = em[Y];
-        const bool wact = (esec >> Y) & 1u;
+        const bool wact = lact && ((esec >> Y) & 1u);
         // the section's erased digits x1 <= x2 (x2 = x1 for one erasure) and its used digits X_j:
         // the three (one erasure) or two (two erasures) X outside E_Y
         x1 = emY ? uint32_t(__builtin_ctz(emY)) : 0u, x2 = emY ? 31u - uint32_t(__builtin_clz(emY)) : 0u;
@@ -266,7 +271,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             total *= nY;
 #pragma unroll
             for (int i = 0; i < IT[y]; i++) {
-                const uint32_t it = uint32_t(lane) + 64u * uint32_t(i);
+                const uint32_t it = uint32_t(lane) + 64u * (uint32_t(i) * nw + part);
                 uint32_t ci = it >> 3;
                 const uint32_t d8 = (it & 7u) * 8u;
                 if (ci >= total) {
@@ -309,10 +314,12 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             }
         });
         };
+        GfTab dinv{0, 0, 0, 0, 0};
         if constexpr (!TWO) {
             setup_one();
         } else {
             setup_two();
+            dinv = load_tab_c(tabc + kDecDetInv * 8);  // (1 + gamma^2)^-1; unset unless a.npair (unused then)
         }
         // ---- the round of iscore level LV + 1 of tile k - 1 (passes [I0, I1) of the lane's items):
         // every target layer z of the level red in section Y adds sum over X != x_e(Y) of
@@ -350,6 +357,35 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         };
+        // ---- the both-erased pairs (two erasures in a section, TWO only): row r at a layer z whose
+        // digit of r's section is its partner's digit holds U after the rounds (the phase-A Out term
+        // needs the erased partner), so C(r, z) = det^-1 (U(r, z) + gamma U(r', z')) and C(r', z') =
+        // det^-1 (U(r', z') + gamma U(r, z)), z' = z with r's digit (get_coupled_from_uncoupled,
+        // decode.rs:228-232, transforms.rs:108-125): 64 layer pairs x 8 pieces per section, both
+        // entries of a pair by one lane (no hand-over between lanes)
+        auto pairs = [&]() BS_INL {
+            const uint32_t gl = uint32_t(li) * 64u + uint32_t(lane);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const uint32_t pi = a.pinfo[r];
+                const uint32_t pr = (pi >> 1) & 3u;
+                if (!(pi & 1u) || pr < uint32_t(r)) continue;  // uniform: each pair once
+                const uint32_t sh = 2u * (3u - ((pi >> 3) & 3u)), xr = (pi >> 5) & 3u, xo = (pi >> 7) & 3u;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t it = gl + 256u * uint32_t(h);
+                    const uint32_t zi = it >> 3, d8 = (it & 7u) * 8u;
+                    // zi: the three other digits; insert the section's digit at bit sh
+                    const uint32_t lo = zi & ((1u << sh) - 1u), hi = (zi >> sh) << (sh + 2u);
+                    const uint32_t z = hi | (xo << sh) | lo, zp = hi | (xr << sh) | lo;
+                    uint2 *q1 = reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + z * 64u + d8);
+                    uint2 *q2 = reinterpret_cast<uint2 *>(scr + pr * BUF + zp * 64u + d8);
+                    const uint2 u1 = *q1, u2 = *q2;
+                    *q1 = make_uint2(gf_mul(u1.x ^ gf_xt(u2.x), dinv), gf_mul(u1.y ^ gf_xt(u2.y), dinv));
+                    *q2 = make_uint2(gf_mul(u2.x ^ gf_xt(u1.x), dinv), gf_mul(u2.y ^ gf_xt(u1.y), dinv));
+                }
+            }
+        };
         constexpr bool TM = (PROBE & 16) != 0;
         uint64_t tm_vm = 0, tm_bar = 0, tm_rnd = 0, tm_end = 0, t0 = 0;
         const uint64_t tm_start = TM ? __builtin_amdgcn_s_memtime() : 0;
@@ -382,6 +418,10 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
                 // PROBE 64: the round at the compute waves' priority (the DMA issue above stays at 3)
                 if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(0);
                 round(IC<y>{});
+                // TWO: every round of tile k - 1 is done (the last, level 4, has no targets with two
+                // erasures in a section: at most three sections hold erasures), so the loaders
+                // invert the both-erased pairs in place before B_r(k)
+                if constexpr (TWO && y == 3) pairs();
                 if constexpr ((PROBE & 64) != 0) __builtin_amdgcn_s_setprio(3);
                 if constexpr (TM) tm_rnd += __builtin_amdgcn_s_memtime() - t0;
             });
@@ -390,7 +430,6 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             // the compute waves are past phase A(k): every ring buffer is free, so the next tile's
             // first RB loads stream during the presolve, the region hand-over and the stores
             if (k + 1u < ntile) issue_upto((k + 1u) * NT + RB);
-            if (TWO && a.npair) lds_barrier();  // B_p(k): the compute lanes read C(k-1) and the pair partners
             if constexpr (TM) tm_end += __builtin_amdgcn_s_memtime() - t0;
         }
         wait_vm0();
@@ -493,61 +532,19 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         }
         // C(k-1) out of the region and S'(k) in: each lane reads, then overwrites, the same 16 x 8
         // bytes (rows r, its four slots' layers, its 8-byte piece), so no lane can overwrite a
-        // byte another lane has yet to read -- no hand-over barrier.  With both-erased pairs
-        // (two erasures in a section) the region holds U, not C, at the pair layers: row r at a
-        // layer z whose digit of r's section is the partner's digit pairs with the partner row at
-        // z[y := r's digit], C = det^-1 (U + gamma U*) (get_coupled_from_uncoupled,
-        // decode.rs:228-232, transforms.rs:108-125); the partner is another lane's entry unless
-        // the section is G, so every lane reads all it needs, then B_p, then the S'(k) writes.
+        // byte another lane has yet to read -- no hand-over barrier (the both-erased pairs of TWO
+        // were inverted in place by the loaders before B_r(k))
         uint2 ov[16];  // [row r][slot g]
         {
             const uint32_t z0 = Kn::layer0(opq(c0));
-            if (!TWO || !a.npair) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    if (uint32_t(r) >= a.ne) continue;
+            for (int r = 0; r < 4; r++) {
+                if (uint32_t(r) >= a.ne) continue;
 #pragma unroll
-                    for (int g = 0; g < 4; g++) {
-                        uint2 *q = reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p);
-                        if (k >= 1) ov[r * 4 + g] = *q;
-                        if (k < ntile) *q = make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
-                    }
-                }
-            } else if constexpr (TWO) {
-                if (k >= 1) {
-                    const GfTab dinv = load_tab_c(tabc + kDecDetInv * 8);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        if (uint32_t(r) >= a.ne) continue;
-                        const uint32_t pi = a.pinfo[r];
-                        const bool haspr = pi & 1u;
-                        const uint32_t pr = (pi >> 1) & 3u, sh = 2u * (3u - ((pi >> 3) & 3u)), xr = (pi >> 5) & 3u,
-                                       xo = (pi >> 7) & 3u;
-#pragma unroll
-                        for (int g = 0; g < 4; g++) {
-                            const uint32_t z = z0 + uint32_t(g) * Kn::wt(G);
-                            ov[r * 4 + g] = *reinterpret_cast<const uint2 *>(scr + uint32_t(r) * BUF + z * 64u + 8u * p);
-                            if (haspr && ((z >> sh) & 3u) == xo) {
-                                const uint32_t zp = (z & ~(3u << sh)) | (xr << sh);
-                                const uint2 u2 =
-                                    *reinterpret_cast<const uint2 *>(scr + pr * BUF + zp * 64u + 8u * p);
-                                const uint2 u1 = ov[r * 4 + g];
-                                ov[r * 4 + g] =
-                                    make_uint2(gf_mul(u1.x ^ gf_xt(u2.x), dinv), gf_mul(u1.y ^ gf_xt(u2.y), dinv));
-                            }
-                        }
-                    }
-                }
-                lds_barrier();  // B_p(k): every lane has read C(k-1) and its pair partners
-                if (k < ntile) {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        if (uint32_t(r) >= a.ne) continue;
-#pragma unroll
-                        for (int g = 0; g < 4; g++)
-                            *reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p) =
-                                make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
-                    }
+                for (int g = 0; g < 4; g++) {
+                    uint2 *q = reinterpret_cast<uint2 *>(scr + uint32_t(r) * BUF + (z0 + uint32_t(g) * Kn::wt(G)) * 64u + 8u * p);
+                    if (k >= 1) ov[r * 4 + g] = *q;
+                    if (k < ntile) *q = make_uint2(S[r * 8 + 2 * g], S[r * 8 + 2 * g + 1]);
                 }
             }
         }

@@ -149,15 +149,18 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, stream_m
         assert np.array_equal(a[e], b[e]), e
 
 
-def f2_fits(c, er):
-    """The host's round-capacity check (engine.hip f2_fits): per section Y with an erasure and
-    iscore level L, the layers with z_Y in E_Y and L erased sections red, <= kF2Iters[L - 1]
-    passes of 64 lanes x 8-byte pieces."""
-    iters = [9, 8, 2, 1]
+def f2_fits(c, er, two=False):
+    """The host's round-capacity check (engine.hip f2_plan): per section Y with an erasure and
+    iscore level L, P(Y, L) = passes of 64 lanes x 8-byte pieces over the layers with z_Y in E_Y
+    and L erased sections red; the four loader waves: one per section with an erasure, the spare
+    ones to the section with the most passes per wave; a wave holds <= kF2Iters (two) / kF2Iters1
+    passes per level."""
+    iters = [5, 4, 2, 1] if two else [6, 4, 2, 1]
     em = [0] * c.t
     for e in er:
         i = _internal(c, e)
         em[i // c.q] |= 1 << (i % c.q)
+    P = {}
     for Y in range(c.t):
         if not em[Y]:
             continue
@@ -167,9 +170,17 @@ def f2_fits(c, er):
                 d = [(z >> (2 * (3 - y))) & 3 for y in range(4)]
                 red = sum(1 for y in range(4) if (em[y] >> d[y]) & 1)
                 n += 1 if (em[Y] >> d[Y]) & 1 and red == L else 0
-            if (n * 8 + 63) // 64 > iters[L - 1]:
-                return False
-    return True
+            P[Y, L] = (n * 8 + 63) // 64
+    act = [y for y in range(c.t) if em[y]]
+    tot = {y: sum(P[y, L] for L in range(1, 5)) for y in act}
+    nw = {y: 1 for y in act}
+    for _ in range(4 - len(act)):
+        best = None
+        for y in act:
+            if best is None or tot[y] * nw[best] > tot[best] * nw[y]:
+                best = y
+        nw[best] += 1
+    return all(-(-P[y, L] // nw[y]) <= iters[L - 1] for y in act for L in range(1, 5))
 
 
 def fused2_eligible(c, er, two=False):
@@ -179,7 +190,7 @@ def fused2_eligible(c, er, two=False):
     per = [0] * c.t
     for e in er:
         per[_internal(c, e) // c.q] += 1
-    if not 2 <= len(er) <= c.t or max(per) > (2 if two else 1) or not f2_fits(c, er):
+    if not 2 <= len(er) <= c.t or max(per) > (2 if two else 1) or not f2_fits(c, er, two):
         return False
     alive = [0] * c.t
     for i in range(c.n):
