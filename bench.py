@@ -359,7 +359,9 @@ def config_legs(torch, dev, local, stream, oracle_cls, calls: int):
     full = rnd((c.n, chunk), 51)
     outs = torch.zeros((c.n, chunk), dtype=torch.uint8, device=dev)
     ins = [None if i in er else full[i] for i in range(c.n)]
-    ous = [outs[i] if i in er else None for i in range(c.n)]
+    # the reference's decode returns the data chunks (decode.rs:167-257): the erased parity chunk
+    # is solved for inside the kernel but not written
+    ous = [outs[i] if i in er and i < c.k else None for i in range(c.n)]
     ms = _event_times(torch, stream, lambda: c.decode_device(ins, er, ous, chunk, local, sh), calls)
     path = clay_amd.last_exec_path()
     o = oracle_cls(10, 4, 13)

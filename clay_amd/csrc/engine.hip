@@ -34,6 +34,7 @@
 #include "stream_encode.hpp"
 #include "repair_args.hpp"  // bit-sliced repair kernel: repair_kernel.hpp, instantiated in repair_stream.hip
 #include "decode_args.hpp"  // streaming-decode kernel: stream_decode.hpp, instantiated in decode_stream.hip
+#include "decode1_args.hpp"  // single-erasure bit-sliced decode: bitslice_decode1.hpp, in decode_bs1.hip
 #include "kernels.hpp"
 #include "plan.hpp"
 #include "tuning.hpp"
@@ -2134,6 +2135,42 @@ static Error decode_by_repair(const clay_code_t &c, const uint8_t *const *chunks
     return Error{};
 }
 
+// Single erasure of a small q = m code without shortened nodes ((4,2,5), BASELINE config 2) with
+// every other chunk present: k_bs_decode1 (bitslice_decode1.hpp), the erased node's whole
+// decode_layered as compile-time XOR networks, one launch.
+static Error launch_bs_decode1(CodeState &cs, const DevProps &prop, const uint8_t *const *chunks, size_t e,
+                               uint8_t *out, size_t chunk, hipStream_t stream, bool *done) {
+    *done = false;
+    const clay_code_t &c = cs.code;
+    const int W = bs_decode1_tile(int(c.k), int(c.m));
+    if (!W || c.d != c.k + c.m - 1 || c.nu != 0 || !out || c.q * c.t > 8) return Error{};
+    const size_t sc = chunk / c.sub_chunk_no;
+    if (sc == 0 || chunk % c.sub_chunk_no) return Error{};
+    using S = bs::Shape<4, 2>;  // the only instantiation (bs_decode1_tile)
+    for (int p = 0; p < 2; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    bs::Dec1Args a{};
+    bool bt = sc % 8 != 0 || (reinterpret_cast<uintptr_t>(out) & 7u) != 0;
+    for (size_t i = 0; i < c.n; i++) {
+        if (i == e) continue;
+        if (!chunks[i]) return Error{};
+        a.node[internal_of(c, i)] = chunks[i];
+        bt |= (reinterpret_cast<uintptr_t>(chunks[i]) & 7u) != 0;
+    }
+    a.out = out;
+    a.sc = sc;
+    a.ntiles = uint32_t((sc + size_t(W) - 1) / size_t(W));
+    a.tiles_per_xcd = (a.ntiles + 7) / 8;
+    a.nslots = std::min(a.tiles_per_xcd, uint32_t(std::max(1, prop.cus / 8) * 8));
+    CLAY_HIP(launch_bs_decode1_kernel(int(c.k), int(c.m), int(internal_of(c, e)), bt, a, stream));
+    t_last_launches += 1;
+    t_last_exec = "bs-decode1";
+    *done = true;
+    return Error{};
+}
+
 static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *chunks, const size_t *er, size_t ner,
                                 uint8_t *const *outs, size_t chunk, int dev, void *stream, bool codeword = false) {
     Error e = check_code(code);
@@ -2189,6 +2226,13 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     if (codeword && (xmode == kExecAuto || xmode == kExecStream) && n_erased == 1 && ner == 1 && ids.size() + 1 == c.n) {
         bool done = false;
         e = decode_by_repair(c, chunks, er[0], outs[er[0]], chunk, dev, static_cast<hipStream_t>(stream), &done);
+        if (e || done) return e;
+    }
+    // one erasure of (4,2,5) with every other chunk present: the bit-sliced single-erasure decode
+    if ((xmode == kExecAuto || xmode == kExecStream) && n_erased == 1 && ner == 1 && ids.size() + 1 == c.n) {
+        bool done = false;
+        e = launch_bs_decode1(cs, dev_props(dev), chunks, er[0], outs[er[0]], chunk, static_cast<hipStream_t>(stream),
+                              &done);
         if (e || done) return e;
     }
     // streaming decodes of q = 4, t = 4 codes (sc % 8 == 0, sc >= 512):

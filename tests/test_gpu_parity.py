@@ -254,10 +254,11 @@ def test_tile_executor_selected(oracle_mod, cfg, lost, mode, launches):
     assert got == o.repair(lost, pr, chunk)
 
 
-@pytest.mark.parametrize("mode,expect", [("auto", "tile"), ("grouped", "grouped"), ("tile", "tile")])
+@pytest.mark.parametrize("mode,expect", [("auto", "bs-decode1"), ("grouped", "grouped"), ("tile", "tile")])
 def test_small_decode_plan_executor(oracle_mod, mode, expect):
-    """(4,2,5) 1-erasure decode is a small two-level plan: auto runs it on the tile-fused
-    executor (one launch); every mode returns the oracle's bytes on random inputs."""
+    """(4,2,5) 1-erasure decode: auto runs the bit-sliced single-erasure kernel (round 6), "tile"
+    the small two-level plan on the tile-fused executor (one launch); every mode returns the
+    oracle's bytes on random inputs."""
     c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
     chunk = c.sub_chunk_no * (16 * 300 + 6)
     chunks = np.random.default_rng(5).integers(0, 256, (c.n, chunk), dtype=np.uint8)
