@@ -1,5 +1,8 @@
-// bitslice_decode1.hpp -- bit-sliced single-erasure decode of small q = m codes without shortened
-// nodes (BASELINE config 2: (4,2,5), alpha = 8), one launch, no LDS: the whole decode_layered of
+// bitslice_line.hpp -- line-local bit-sliced kernels for small q = m codes without shortened nodes
+// (BASELINE config 2: (4,2,5), alpha = 8): a lane owns 32 positions of one "line" of q layers and
+// everything a line needs stays in its registers -- no LDS, no barriers.
+//
+// k_bs_decode1: single-erasure decode, one launch: the whole decode_layered of
 // one erasure (decode.rs:167-257) is a fixed GF(2^8)-linear map per byte position, so the erased
 // node E is a template parameter and every coefficient is a compile-time XOR network.
 //
@@ -23,7 +26,7 @@
 #pragma once
 
 #include "bitslice.hpp"
-#include "decode1_args.hpp"
+#include "line_args.hpp"
 
 namespace clay {
 namespace bs {
@@ -205,6 +208,118 @@ __global__ __launch_bounds__((Dec1Kernel<KD, M, E, PG>::BLOCK)) void k_bs_decode
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
     for (uint32_t tix = slot; tix < a.tiles_per_xcd; tix += a.nslots) {
         const uint32_t tile = xcd * a.tiles_per_xcd + tix;  // each XCD streams a contiguous run
+        if (tile >= a.ntiles) break;
+        const uint64_t b0 = uint64_t(tile) * Kn::W;
+        if (b0 + Kn::W <= a.sc) Kn::template tile<true, BT>(a, b0);
+        else Kn::template tile<false, BT>(a, b0);
+    }
+}
+
+// ---------------- k_bs_encode1: the encode, one line per lane ----------------
+// (encode.rs:30-80 -> decode_layered with every parity node erased, decode.rs:167-257: one iscore
+// level.)  Lane = 32 positions of the q layers z0 + j (j = the parity section's digit, weight 1):
+// per layer, U_i = C_i + gamma C_i* for the data nodes (transforms.rs:42-55; companions of other
+// lines read directly), V_p += g_(p,i) U_i (the RS parity rows, compile time), then the parity
+// section's PFT pairs (transforms.rs:108-125) -- node (T-1, x) at layer z0 + j pairs with (T-1, j)
+// at z0 + x, in the same line -- and the stores.  The same linear map as k_bs_encode (bitslice.hpp),
+// whose V accumulators go through LDS because its lanes split a line.
+template <int KD, int M, int PG>
+struct Enc1Kernel {
+    using S = Shape<KD, M>;
+    static_assert(S::NU == 0 && S::N <= 8, "small codes without shortened nodes");
+    static constexpr int Q = S::Q, T = S::T, ALPHA = S::ALPHA;
+    static constexpr int LINES = ALPHA / Q, UNITS = LINES * PG, BLOCK = UNITS < 1024 ? UNITS : 1024;
+    static constexpr int W = 32 * PG;  // positions per tile
+    static constexpr int wt(int y) {
+        int w = 1;
+        for (int i = 0; i < T - 1 - y; i++) w *= Q;
+        return w;
+    }
+    template <uint8_t CF>
+    __device__ __forceinline__ static void fold(uint32_t (&acc)[8], const uint32_t (&v)[8]) {
+        if constexpr (CF != 0) {
+            sfor<8>([&](auto bc) BS_INL {
+                constexpr int bo = decltype(bc)::value;
+                acc[bo] = xor_sel<plane_mask(CF, bo, 0), true>(acc[bo], v);
+            });
+        }
+    }
+
+    template <bool FULL, bool BT>
+    __device__ static void tile(const Enc1Args &a, uint64_t b0) {
+        for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
+            const int pg = u % PG, line = u / PG;
+            const uint32_t z0 = uint32_t(line * Q);
+            const uint64_t pos = b0 + uint64_t(32 * pg);
+            const int nv = FULL ? (BT ? 32 : 4)
+                         : BT ? int(pos >= a.sc ? 0 : a.sc - pos > 32 ? 32 : a.sc - pos)                // bytes
+                              : int(pos >= a.sc ? 0 : (a.sc - pos) / 8 > 4 ? 4 : (a.sc - pos) / 8);  // pieces
+            uint32_t V[Q][M][8];  // [layer j of the line][parity node p][plane]: U of the parity nodes
+            sfor<Q>([&](auto jc) BS_INL {
+                constexpr int j = decltype(jc)::value;
+                const uint32_t z = z0 + uint32_t(j);
+#pragma unroll
+                for (int p = 0; p < M; p++)
+#pragma unroll
+                    for (int w = 0; w < 8; w++) V[j][p][w] = 0;
+                sfor<KD>([&](auto ic) BS_INL {
+                    constexpr int i = decltype(ic)::value;
+                    constexpr int yi = i / Q, xi = i % Q;
+                    uint32_t o[8], cv[8], t[8];
+                    ld32<FULL, BT>(o, a.data[i] + uint64_t(z) * a.sc + pos, nv);
+                    // companion (yi, d) at z[yi := xi], d = z's digit yi (the line's)
+                    const int d = int(z / uint32_t(wt(yi))) % Q;
+                    const uint8_t *cn = a.data[yi * Q];
+#pragma unroll
+                    for (int xx = 1; xx < Q; xx++) cn = d == xx ? a.data[yi * Q + xx] : cn;
+                    const uint32_t zc = uint32_t(int(z) + (xi - d) * wt(yi));
+                    ld32<FULL, BT>(cv, cn + uint64_t(zc) * a.sc + pos, nv);
+                    const uint32_t keep = d != xi ? 0xffffffffu : 0u;
+                    const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
+#pragma unroll
+                    for (int w = 0; w < 8; w++) t[w] = xor_xtime4_masked(o[w], cv[w], ks, kr);
+                    transpose8(t);
+                    sfor<M>([&](auto pc) BS_INL {
+                        constexpr int p = decltype(pc)::value;
+                        fold<S::RS.g[p][i]>(V[j][p], t);
+                    });
+                });
+            });
+            // PFT: C(x, z0 + j) = det^-1 (V(x, z0 + j) + gamma V(j, z0 + x)); red (x == j): C = V
+            sfor<Q>([&](auto jc) BS_INL {
+                constexpr int j = decltype(jc)::value;
+                sfor<M>([&](auto xc) BS_INL {
+                    constexpr int x = decltype(xc)::value;
+                    uint32_t c[8];
+                    if constexpr (x == j) {
+#pragma unroll
+                        for (int w = 0; w < 8; w++) c[w] = V[j][x][w];
+                    } else {
+                        uint32_t in[16];
+#pragma unroll
+                        for (int w = 0; w < 8; w++) {
+                            in[w] = V[j][x][w];
+                            in[8 + w] = V[x][j][w];
+                        }
+                        sfor<8>([&](auto bc) BS_INL {
+                            constexpr int bo = decltype(bc)::value;
+                            c[bo] = xor_sel<plane_mask(S::DINV, bo, 0) | plane_mask(gm(S::DINV, 2), bo, 8), false>(0u, in);
+                        });
+                    }
+                    transpose8(c);
+                    st32<FULL, BT>(a.par[x] + uint64_t(z0 + uint32_t(j)) * a.sc + pos, c, nv);
+                });
+            });
+        }
+    }
+};
+
+template <int KD, int M, int PG, bool BT = false>
+__global__ __launch_bounds__((Enc1Kernel<KD, M, PG>::BLOCK)) void k_bs_encode1(Enc1Args a) {
+    using Kn = Enc1Kernel<KD, M, PG>;
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    for (uint32_t tix = slot; tix < a.tiles_per_xcd; tix += a.nslots) {
+        const uint32_t tile = xcd * a.tiles_per_xcd + tix;
         if (tile >= a.ntiles) break;
         const uint64_t b0 = uint64_t(tile) * Kn::W;
         if (b0 + Kn::W <= a.sc) Kn::template tile<true, BT>(a, b0);

@@ -34,7 +34,7 @@
 #include "stream_encode.hpp"
 #include "repair_args.hpp"  // bit-sliced repair kernel: repair_kernel.hpp, instantiated in repair_stream.hip
 #include "decode_args.hpp"  // streaming-decode kernel: stream_decode.hpp, instantiated in decode_stream.hip
-#include "decode1_args.hpp"  // single-erasure bit-sliced decode: bitslice_decode1.hpp, in decode_bs1.hip
+#include "line_args.hpp"  // line-local bit-sliced (4,2,5) encode / single-erasure decode: bitslice_line.hpp, in line_kernels.hip
 #include "kernels.hpp"
 #include "plan.hpp"
 #include "tuning.hpp"
@@ -1450,6 +1450,43 @@ static Error launch_stream3(CodeState &cs, const DevProps &prop, const uint8_t *
     return Error{};
 }
 
+// (4,2,5) on the line-local bit-sliced encode (bitslice_line.hpp: no LDS, one launch per stripe)
+static Error launch_bs_encode1(CodeState &cs, const DevProps &prop, const uint8_t *const *data, uint8_t *const *par,
+                               size_t n_stripes, size_t sc, hipStream_t stream, bool *done) {
+    *done = false;
+    const clay_code_t &c = cs.code;
+    const int W = bs_decode1_tile(int(c.k), int(c.m));  // the line kernels' tile (same lane map)
+    if (!W || c.d != c.k + c.m - 1 || c.nu != 0 || sc == 0) return Error{};
+    using S = bs::Shape<4, 2>;
+    for (int p = 0; p < 2; p++)
+        for (int i = 0; i < S::K; i++)
+            if (S::RS.g[p][i] != cs.rs.gen[(S::K + p) * S::K + i])
+                return make_error(CLAY_ERR_DEVICE, 0, 0, 0, "bit-sliced RS table mismatch");
+    for (size_t s = 0; s < n_stripes; s++) {
+        bs::Enc1Args a{};
+        bool bt = sc % 8 != 0;
+        for (size_t i = 0; i < c.k; i++) {
+            a.data[i] = data[s * c.k + i];
+            bt |= (reinterpret_cast<uintptr_t>(a.data[i]) & 7u) != 0;
+        }
+        for (size_t x = 0; x < c.m; x++) {
+            a.par[x] = par[s * c.m + x];
+            bt |= (reinterpret_cast<uintptr_t>(a.par[x]) & 7u) != 0;
+        }
+        a.sc = sc;
+        a.ntiles = uint32_t((sc + size_t(W) - 1) / size_t(W));
+        a.tiles_per_xcd = (a.ntiles + 7) / 8;
+        a.nslots = std::min(a.tiles_per_xcd, uint32_t(std::max(1, prop.cus / 8) * 8));
+        CLAY_HIP(launch_bs_encode1_kernel(int(c.k), int(c.m), bt, a, stream));
+        t_last_launches++;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "bitsliced-line-k%zum%zu-w%d", c.k, c.m, W);
+    t_last_path = buf;
+    *done = true;
+    return Error{};
+}
+
 static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data, uint8_t *const *par,
                               size_t n_stripes, size_t chunk, hipStream_t stream, int mode, int tile, bool *done) {
     *done = false;
@@ -1485,6 +1522,11 @@ static Error encode_bitsliced(CodeState &cs, int dev, const uint8_t *const *data
                 e = launch_stream<9, 4>(cs, prop, data, par, n_stripes, sc, stream, done);
         }
         if (e || *done || mode == kModeStream) return e;
+    }
+    // (4,2,5): the line-local kernel (auto and "stream"; "bitsliced" keeps the v1 kernel for A/B)
+    if (key == 402 && (mode == kModeStream || mode == kModeAuto)) {
+        e = launch_bs_encode1(cs, prop, data, par, n_stripes, sc, stream, done);
+        if (e || *done) return e;
     }
     if (mode == kModeStream) return e;
     // v1 (register loads, PG x 32 positions per lane): every q = m code it is instantiated for
@@ -2136,7 +2178,7 @@ static Error decode_by_repair(const clay_code_t &c, const uint8_t *const *chunks
 }
 
 // Single erasure of a small q = m code without shortened nodes ((4,2,5), BASELINE config 2) with
-// every other chunk present: k_bs_decode1 (bitslice_decode1.hpp), the erased node's whole
+// every other chunk present: k_bs_decode1 (bitslice_line.hpp), the erased node's whole
 // decode_layered as compile-time XOR networks, one launch.
 static Error launch_bs_decode1(CodeState &cs, const DevProps &prop, const uint8_t *const *chunks, size_t e,
                                uint8_t *out, size_t chunk, hipStream_t stream, bool *done) {

@@ -1,6 +1,6 @@
-// decode_bs1.hip -- instantiations and launcher of the single-erasure bit-sliced decode
-// (bitslice_decode1.hpp): (4,2,5), every erased node.
-#include "bitslice_decode1.hpp"
+// line_kernels.hip -- instantiations and launchers of the line-local bit-sliced kernels
+// (bitslice_line.hpp) for (4,2,5): the encode and the single-erasure decode of every node.
+#include "bitslice_line.hpp"
 
 namespace clay {
 
@@ -27,6 +27,16 @@ hipError_t launch_bs_decode1_kernel(int k, int m, int e, bool bt, const bs::Dec1
         case 5: return launch42<5>(bt, a, stream);
         default: break;
         }
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_bs_encode1_kernel(int k, int m, bool bt, const bs::Enc1Args &a, hipStream_t stream) {
+    if (k == 4 && m == 2) {
+        using Kn = bs::Enc1Kernel<4, 2, kPg>;
+        if (bt) bs::k_bs_encode1<4, 2, kPg, true><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+        else bs::k_bs_encode1<4, 2, kPg><<<dim3(a.nslots * 8), dim3(Kn::BLOCK), 0, stream>>>(a);
+        return hipGetLastError();
     }
     return hipErrorInvalidValue;
 }

@@ -60,7 +60,17 @@ def rnd(n, chunk, seed):
     return torch.randint(0, 256, (n, chunk), dtype=torch.uint8, device="cuda", generator=g)
 
 
-def encode_cfg(k, m, d, stripe):
+def encode_cfg(k, m, d, stripe, path=None):
+    if path:
+        clay_amd.set_encode_path(path, 0)
+    try:
+        _encode_cfg(k, m, d, stripe)
+    finally:
+        if path:
+            clay_amd.set_encode_path("auto", 0)
+
+
+def _encode_cfg(k, m, d, stripe):
     c = ClayCode(k, m, d)
     chunk = c.encoded_chunk_size(stripe)
     data, par = rnd(k, chunk, 1), torch.empty((m, chunk), dtype=torch.uint8, device="cuda")
@@ -154,6 +164,8 @@ if __name__ == "__main__":
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),
             ("decode", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12], "grouped")),
             ("cfg5", lambda: decode_cfg(10, 4, 13, 1 << 30, [0, 4, 8, 12])),  # under CLAY_EXEC
+            ("c2e", lambda: encode_cfg(4, 2, 5, 64 << 20)),
+            ("c2e", lambda: encode_cfg(4, 2, 5, 64 << 20, "bitsliced")),
             ("cfg2", lambda: decode_cfg(4, 2, 5, 64 << 20, [0])),  # under CLAY_EXEC
             ("cfg2", lambda: decode_cfg(4, 2, 5, 64 << 20, [5])),
             # the fused decode v2 for 3 and 2 erasures in distinct sections (auto: split / local)

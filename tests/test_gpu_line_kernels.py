@@ -1,5 +1,5 @@
-"""GPU parity of the single-erasure bit-sliced decode k_bs_decode1 (bitslice_decode1.hpp) for
-(4,2,5), BASELINE config 2, against the oracle.
+"""GPU parity of the line-local bit-sliced kernels (bitslice_line.hpp) for (4,2,5), BASELINE
+config 2, against the oracle: the encode k_bs_encode1 and the single-erasure decode k_bs_decode1.
 
 Inputs are random (not codewords) for the erased data nodes: only the reference's exact RS row
 choice (reconstruct from the first k present shards, decode.rs:374) and its iscore order reproduce
@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import clay_amd
-from clay_amd import ClayCode
+from clay_amd import ClayCode, last_encode_path, set_encode_path
 
 pytestmark = pytest.mark.gpu
 
@@ -106,3 +106,65 @@ def test_decode1_config2_full_size_codeword(oracle_mod, torch_cuda):
         s = np.ascontiguousarray(host[:, :, p0:p0 + 64]).reshape(c.n, -1)
         ref = np.frombuffer(o.decode({i: s[i] for i in range(1, c.n)}, [0]), np.uint8).reshape(c.k, -1)
         assert np.array_equal(got[:, p0:p0 + 64].reshape(-1), ref[0]), p0
+
+
+# the oracle pads a sub-chunk to an even length (encode.rs:33-39): even sc for the encode
+ENC_SC = [2048 * 3, 2048 + 8 * 37, 16, 2048 * 2 + 6, 778]
+
+
+@pytest.mark.parametrize("sc", ENC_SC)
+def test_encode1_matches_oracle(oracle_mod, sc):
+    """Auto mode runs k_bs_encode1 for (4,2,5): whole tiles, a partial last tile, byte tails
+    (sc % 8 != 0), bit-exact against the oracle; "bitsliced" still selects the v1 kernel."""
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    data = np.random.default_rng(sc).integers(0, 256, c.k * c.sub_chunk_no * sc, dtype=np.uint8).tobytes()
+    ref = o.encode_array(data)
+    assert ref.shape[1] == c.sub_chunk_no * sc
+    got = c.encode_array(data)
+    assert last_encode_path().startswith("bitsliced-line"), last_encode_path()
+    assert np.array_equal(got, ref), sc
+    set_encode_path("bitsliced", 0)
+    try:
+        v1 = c.encode_array(data)
+        assert last_encode_path().startswith("bitsliced-k4m2"), last_encode_path()
+    finally:
+        set_encode_path("auto", 0)
+    assert np.array_equal(v1, ref)
+
+
+@pytest.mark.parametrize("off", [1, 6])
+def test_encode1_unaligned_chunks(oracle_mod, torch_cuda, off):
+    """Chunk pointers off 8-byte alignment take the byte-tail instantiation."""
+    torch = torch_cuda
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    sc = 2048 + 40
+    chunk = c.sub_chunk_no * sc
+    data = np.random.default_rng(off).integers(0, 256, c.k * chunk, dtype=np.uint8)
+    ref = o.encode_array(data.tobytes())
+    buf = torch.zeros((c.n, chunk + off), dtype=torch.uint8, device="cuda")
+    buf[:c.k, off:] = torch.from_numpy(data.reshape(c.k, chunk)).cuda()
+    c.encode_device([buf[i, off:] for i in range(c.k)], [buf[c.k + x, off:] for x in range(c.m)], chunk)
+    torch.cuda.synchronize()
+    assert last_encode_path().startswith("bitsliced-line"), last_encode_path()
+    assert np.array_equal(buf[c.k:, off:].cpu().numpy(), ref[c.k:])
+
+
+def test_encode1_config2_full_size_slices(oracle_mod, torch_cuda):
+    """BASELINE config 2's 64 MiB stripe: column slices of the parity match the oracle's encode of
+    the same slices (positions [p0, p0 + 64) of every sub-chunk are an independent codeword)."""
+    torch = torch_cuda
+    c, o = ClayCode(4, 2, 5), oracle_mod.OracleClay(4, 2, 5)
+    chunk = c.encoded_chunk_size(64 << 20)
+    sc = chunk // c.sub_chunk_no
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    full = torch.zeros((c.n, chunk), dtype=torch.uint8, device="cuda")
+    full[:c.k] = torch.randint(0, 256, (c.k, chunk), dtype=torch.uint8, device="cuda", generator=g)
+    c.encode_device([full[i] for i in range(c.k)], [full[c.k + x] for x in range(c.m)], chunk)
+    torch.cuda.synchronize()
+    assert last_encode_path().startswith("bitsliced-line"), last_encode_path()
+    host = full.view(c.n, c.sub_chunk_no, sc).cpu().numpy()
+    for p0 in (0, sc // 2 + 8, sc - 64):
+        s = np.ascontiguousarray(host[:, :, p0:p0 + 64]).reshape(c.n, -1)
+        ref = o.encode_array(s[:c.k].reshape(-1).tobytes())
+        assert np.array_equal(s[c.k:], ref[c.k:]), p0
