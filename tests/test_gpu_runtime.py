@@ -97,9 +97,12 @@ def test_host_api_concurrent_threads(oracle_mod, torch_cuda):
     assert not errors, errors
 
 
-@pytest.mark.parametrize("er,path", [([1, 2, 5, 6], "grouped"), ([0, 4, 8, 12], "stream-fused2")])
-def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path):
-    prev = clay_amd.set_exec_mode("auto")
+# (round 6: every 2-4 erasure pattern of (10,4,13) streams in auto, so the grouped executor's
+# workspace is exercised under exec mode "grouped")
+@pytest.mark.parametrize("er,path,mode", [([1, 2, 5, 6], "grouped", "grouped"), ([1, 2, 5, 6], "stream-fused2", "auto"),
+                                          ([0, 4, 8, 12], "stream-fused2", "auto")])
+def test_workspace_pool_reused_across_streams(oracle_mod, torch_cuda, er, path, mode):
+    prev = clay_amd.set_exec_mode(mode)
     try:
         _workspace_pool_reuse(oracle_mod, torch_cuda, er, path)
     finally:
