@@ -30,7 +30,8 @@ if args.what == "decode4":
     full = torch.randint(0, 256, (c.n, chunk), dtype=torch.uint8, device="cuda")
     outs = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
     ins = [None if i in er else full[i] for i in range(c.n)]
-    ous = [outs[i] if i in er else None for i in range(c.n)]
+    # DATA_ONLY=1: outputs for the erased data chunks only (what the reference's decode returns)
+    ous = [outs[i] if i in er and (i < c.k or not os.environ.get("DATA_ONLY")) else None for i in range(c.n)]
     fn = lambda: c.decode_device(ins, er, ous, chunk)  # noqa: E731
 else:
     c = ClayCode(9, 3, 11)

@@ -323,3 +323,40 @@ def test_fused2_two_erasures_in_a_section_codeword_and_grouped(oracle_mod, torch
             clay_amd.set_exec_mode(prev)
         for e in er:
             assert np.array_equal(a[e], b[e]), (er, e)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("er", [[0, 1, 4, 8], [0, 1, 4, 5], [8, 9, 0, 4], [0, 1, 4, 12]])
+def test_two_in_a_section_1GiB(oracle_mod, torch_cuda, er):
+    """(2,1,1) / (2,2) patterns at the BASELINE stripe (sc 419,432) under auto (k_stream_fused2,
+    TWO): on random chunks, column slices of every erased data chunk match the oracle's decode of
+    the same slices (positions [p0, p0 + 64) of every sub-chunk are an independent instance); on a
+    codeword (the product encode) every erased chunk, parity included, comes back."""
+    torch = torch_cuda
+    c, o = ClayCode(10, 4, 13), oracle_mod.OracleClay(10, 4, 13)
+    chunk = c.encoded_chunk_size(1 << 30)
+    sc = chunk // c.sub_chunk_no
+    g = torch.Generator(device="cuda")
+    g.manual_seed(sum(er))
+    full = torch.randint(0, 256, (c.n, chunk), dtype=torch.uint8, device="cuda", generator=g)
+    outs = torch.zeros((c.n, chunk), dtype=torch.uint8, device="cuda")
+    c.decode_device([None if i in er else full[i] for i in range(c.n)], er,
+                    [outs[i] if i in er and i < c.k else None for i in range(c.n)], chunk)
+    torch.cuda.synchronize()
+    assert clay_amd.last_exec_path() == "stream-fused2"
+    for p0 in (0, sc // 2 + 8, sc - 64):
+        s = full[:, :].view(c.n, c.sub_chunk_no, sc)[:, :, p0:p0 + 64].cpu().numpy().reshape(c.n, -1)
+        got = outs.view(c.n, c.sub_chunk_no, sc)[:, :, p0:p0 + 64].cpu().numpy().reshape(c.n, -1)
+        ref = np.frombuffer(o.decode({i: s[i] for i in range(c.n) if i not in er}, er), np.uint8).reshape(c.k, -1)
+        for e in er:
+            if e < c.k:
+                assert np.array_equal(got[e], ref[e]), (er, p0, e)
+    # codeword: the product encode (oracle-checked by the encode tests), then decode
+    c.encode_device([full[i] for i in range(c.k)], [full[c.k + x] for x in range(c.m)], chunk)
+    outs.zero_()
+    c.decode_device([None if i in er else full[i] for i in range(c.n)], er,
+                    [outs[i] if i in er else None for i in range(c.n)], chunk)
+    torch.cuda.synchronize()
+    assert clay_amd.last_exec_path() == "stream-fused2"
+    for e in er:
+        assert torch.equal(outs[e], full[e]), (er, e)
