@@ -2029,8 +2029,8 @@ hipError_t launch_stream_fused2_kernel(int kd, const bs::DecArgs &a, hipStream_t
 // Rounds of k_stream_fused2 (stream_fused2.hpp): per section Y with an erasure and iscore level L,
 // the targets are the layers z with z_Y in E_Y and exactly L - 1 other sections y with z_y in E_y,
 // P(Y, L) = ceil(targets x 8 / 64) passes of 64 lanes x (8-byte piece).  The four loader waves share
-// them: each section with an erasure gets one wave, the spare waves go one by one to the section
-// with the most passes per wave (ties: the lower section), and a section's nw waves take every
+// them: each section with an erasure gets at least one wave, the spare waves go where they cut
+// the sum over levels of the busiest wave's passes most, and a section's nw waves take every
 // nw-th pass.  f2_plan packs, per loader wave li, byte li of a.lwave: bits 0-1 its section, 2-3 its
 // part, 4-5 nw - 1, bit 6 set (no section: 0); false when a wave would hold more than the kernel's
 // kF2Iters (TWO) / kF2Iters1 passes of some level.
@@ -2050,25 +2050,46 @@ static uint32_t f2_targets(const uint32_t (&emask)[4], int Y, int L) {
     return n;
 }
 static bool f2_plan(const uint32_t (&emask)[4], bool two, uint32_t *lwave) {
-    uint32_t P[4][4] = {}, tot[4] = {}, nw[4] = {};
+    uint32_t P[4][4] = {}, nw[4] = {};
     int nact = 0;
     for (int Y = 0; Y < 4; Y++) {
         if (!emask[Y]) continue;
         nact++;
         nw[Y] = 1;
-        for (int L = 1; L <= 4; L++) {
-            P[Y][L - 1] = (f2_targets(emask, Y, L) * 8u + 63u) / 64u;
-            tot[Y] += P[Y][L - 1];
-        }
-    }
-    for (int s = nact; s < 4; s++) {
-        int best = -1;
-        for (int Y = 0; Y < 4; Y++)  // tot[Y] / nw[Y] > tot[best] / nw[best]
-            if (nw[Y] && (best < 0 || tot[Y] * nw[best] > tot[best] * nw[Y])) best = Y;
-        if (best < 0) break;
-        nw[best]++;
+        for (int L = 1; L <= 4; L++) P[Y][L - 1] = (f2_targets(emask, Y, L) * 8u + 63u) / 64u;
     }
     const int *cap = two ? bs::kF2Iters : bs::kF2Iters1;
+    // the spare waves: the split (every active section >= 1 wave, 4 in all) with the smallest sum
+    // over levels of the busiest wave's passes (each level's round is one step) among those within
+    // the kernel's item registers, first in lexicographic order of (nw[0], .., nw[3]) among equals
+    if (nact > 0 && nact < 4) {
+        uint32_t best[4] = {0, 0, 0, 0}, bcost = ~0u;
+        for (uint32_t n0 = 0; n0 <= 4; n0++)
+            for (uint32_t n1 = 0; n1 <= 4; n1++)
+                for (uint32_t n2 = 0; n2 <= 4; n2++)
+                    for (uint32_t n3 = 0; n3 <= 4; n3++) {
+                        const uint32_t n[4] = {n0, n1, n2, n3};
+                        if (n0 + n1 + n2 + n3 != 4) continue;
+                        bool ok = true;
+                        for (int Y = 0; Y < 4; Y++) ok = ok && ((n[Y] > 0) == (nw[Y] > 0));
+                        if (!ok) continue;
+                        uint32_t cost = 0;
+                        for (int L = 0; L < 4; L++) {
+                            uint32_t mx = 0;
+                            for (int Y = 0; Y < 4; Y++)
+                                if (n[Y]) mx = std::max(mx, (P[Y][L] + n[Y] - 1u) / n[Y]);
+                            if (mx > uint32_t(cap[L])) ok = false;  // over the kernel's item registers
+                            cost += mx;
+                        }
+                        if (!ok) continue;
+                        if (cost < bcost) {
+                            bcost = cost;
+                            for (int Y = 0; Y < 4; Y++) best[Y] = n[Y];
+                        }
+                    }
+        if (bcost == ~0u) return false;  // no split within the item registers
+        for (int Y = 0; Y < 4; Y++) nw[Y] = best[Y];
+    }
     uint32_t pack = 0;
     int li = 0;
     for (int Y = 0; Y < 4; Y++) {
@@ -2287,6 +2308,19 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
     const bool stream_all = xmode == kExecStream;
     const bool try_local = xmode == kExecAuto || stream_all || xmode == kExecStreamLocal;
     const bool try_f2 = xmode == kExecStreamFused2 || stream_all || (xmode == kExecAuto && n_erased >= 3);
+    // (2,1) sections (two erasures in one section, one in another): the fused decode v2 first --
+    // 0.48-0.53 ms vs 0.50-0.54 on the 64-byte local decode (profiles/r06/decode/two_small_*)
+    bool f2_first = false;
+    if (try_f2 && try_local && n_erased == 3 && tn == 16) {
+        int per[4] = {0, 0, 0, 0};
+        for (size_t in = 0; in < tn; in++) per[in / 4] += erased[in] ? 1 : 0;
+        int nsec = 0, mx = 0;
+        for (int y = 0; y < 4; y++) {
+            nsec += per[y] ? 1 : 0;
+            mx = std::max(mx, per[y]);
+        }
+        f2_first = nsec == 2 && mx == 2;
+    }
     if ((try_local || try_f2) && tn == 16) {
         const uint8_t *cin[16] = {};
         uint8_t *cout[16] = {};
@@ -2299,12 +2333,17 @@ static Error decode_device_impl(const clay_code_t *code, const uint8_t *const *c
         const DevProps &prop = dev_props(dev);
         const size_t sc = chunk / c.sub_chunk_no;
         hipStream_t st = static_cast<hipStream_t>(stream);
+        if (f2_first) {
+            if (c.k == 10) e = launch_stream_fused2<10>(cs, prop, cin, cout, erased, sc, st, &done);
+            else if (c.k == 9) e = launch_stream_fused2<9>(cs, prop, cin, cout, erased, sc, st, &done);
+            if (e || done) return e;
+        }
         if (try_local) {
             if (c.k == 10) e = launch_stream_local<10>(cs, prop, cin, cout, erased, sc, st, &done);
             else if (c.k == 9) e = launch_stream_local<9>(cs, prop, cin, cout, erased, sc, st, &done);
             if (e || done) return e;
         }
-        if (try_f2) {
+        if (try_f2 && !f2_first) {
             if (c.k == 10) e = launch_stream_fused2<10>(cs, prop, cin, cout, erased, sc, st, &done);
             else if (c.k == 9) e = launch_stream_fused2<9>(cs, prop, cin, cout, erased, sc, st, &done);
             if (e || done) return e;

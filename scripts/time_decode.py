@@ -19,6 +19,8 @@ chunk = c.encoded_chunk_size(1 << 30)
 full = torch.randint(0, 256, (c.n, chunk), dtype=torch.uint8, device="cuda")
 outs = torch.empty((c.n, chunk), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream()
+if os.environ.get("EXEC"):  # exec mode for the whole run (auto, stream-fused2, stream-local, grouped, ...)
+    clay_amd.set_exec_mode(os.environ["EXEC"])
 lib = os.path.basename(os.environ.get("CLAY_AMD_LIB", "libclay_amd.so"))
 for er in pats:
     ins = [None if i in er else full[i] for i in range(c.n)]

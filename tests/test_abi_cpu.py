@@ -35,7 +35,8 @@ def test_library_exports_every_declared_symbol():
 
 
 SHIPPING_KERNELS = {"k_stream_encode", "k_stream_local", "k_stream_local256", "k_stream_fused2", "k_stream_encode3", "k_bs_repair",
-                    "k_bs_repair_stream", "k_bs_encode", "k_fused_encode", "k_gexec", "k_texec", "k_ygroup"}
+                    "k_bs_repair_stream", "k_bs_encode", "k_bs_encode1", "k_bs_decode1", "k_fused_encode", "k_gexec", "k_texec",
+                    "k_ygroup"}
 
 
 def kernel_names(blob: bytes):

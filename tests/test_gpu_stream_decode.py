@@ -49,6 +49,9 @@ def local_eligible(c, er):
 
 def stream_path(c, er):
     """The kernel exec mode "stream" runs a pattern on (None: the plan executor)."""
+    per = sorted((sum(1 for e in er if _internal(c, e) // c.q == y) for y in range(c.t)), reverse=True)
+    if len(er) == 3 and per[:2] == [2, 1] and fused2_eligible(c, er, two=True):
+        return "stream-fused2"  # (2,1) sections: the fused decode v2 first (round 6)
     if local_eligible(c, er):
         per = [0] * c.t
         for e in er:
@@ -152,9 +155,9 @@ def test_stream_decode_matches_grouped_executor(oracle_mod, torch_cuda, stream_m
 def f2_fits(c, er, two=False):
     """The host's round-capacity check (engine.hip f2_plan): per section Y with an erasure and
     iscore level L, P(Y, L) = passes of 64 lanes x 8-byte pieces over the layers with z_Y in E_Y
-    and L erased sections red; the four loader waves: one per section with an erasure, the spare
-    ones to the section with the most passes per wave; a wave holds <= kF2Iters (two) / kF2Iters1
-    passes per level."""
+    and L erased sections red; the four loader waves: at least one per section with an erasure,
+    split to minimise the sum over levels of the busiest wave's passes; a wave holds <= kF2Iters
+    (two) / kF2Iters1 passes per level."""
     iters = [5, 4, 2, 1] if two else [6, 4, 2, 1]
     em = [0] * c.t
     for e in er:
@@ -172,15 +175,17 @@ def f2_fits(c, er, two=False):
                 n += 1 if (em[Y] >> d[Y]) & 1 and red == L else 0
             P[Y, L] = (n * 8 + 63) // 64
     act = [y for y in range(c.t) if em[y]]
-    tot = {y: sum(P[y, L] for L in range(1, 5)) for y in act}
-    nw = {y: 1 for y in act}
-    for _ in range(4 - len(act)):
-        best = None
-        for y in act:
-            if best is None or tot[y] * nw[best] > tot[best] * nw[y]:
-                best = y
-        nw[best] += 1
-    return all(-(-P[y, L] // nw[y]) <= iters[L - 1] for y in act for L in range(1, 5))
+    best, bcost = None, None
+    for n in itertools.product(range(5), repeat=4):  # lexicographic, as the host's loops
+        if sum(n) != 4 or any((n[y] > 0) != (y in act) for y in range(4)):
+            continue
+        mx = [max(-(-P[y, L] // n[y]) for y in act) for L in range(1, 5)]
+        if any(m > iters[L] for L, m in enumerate(mx)):
+            continue
+        cost = sum(mx)
+        if bcost is None or cost < bcost:
+            best, bcost = n, cost
+    return best is not None
 
 
 def fused2_eligible(c, er, two=False):
@@ -360,3 +365,29 @@ def test_two_in_a_section_1GiB(oracle_mod, torch_cuda, er):
     assert clay_amd.last_exec_path() == "stream-fused2"
     for e in er:
         assert torch.equal(outs[e], full[e]), (er, e)
+
+
+@pytest.mark.parametrize("cfg", [(10, 4, 13), (9, 4, 12)])
+@pytest.mark.parametrize("sc", [520, 64 * 37 + 40])
+def test_fused2_two_erasures_small_patterns(oracle_mod, torch_cuda, cfg, sc):
+    """Exec mode "stream-fused2" on 2- and 3-erasure patterns with two erasures in a section
+    ((2) and (2,1) sections: the loader-wave plan gives the busy section 3-4 waves), random
+    chunks, erased data chunks bit-exact vs the oracle."""
+    torch = torch_cuda
+    c, o = ClayCode(*cfg), oracle_mod.OracleClay(*cfg)
+    chunk = c.sub_chunk_no * sc
+    rng = np.random.default_rng(sc + cfg[0])
+    pats = [[0, 1], [2, 3], [0, 1, 4], [0, 4, 5], [c.n - 2, c.n - 1, 0], [c.n - 1, 1, 2]]
+    prev = clay_amd.set_exec_mode("stream-fused2")
+    try:
+        for er in pats:
+            assert fused2_eligible(c, er, two=True), er
+            chunks = rng.integers(0, 256, (c.n, chunk), dtype=np.uint8)
+            got = _decode_dev(torch, c, chunks, er, chunk, want_parity=False)
+            assert clay_amd.last_exec_path() == "stream-fused2", (er, clay_amd.last_exec_path())
+            ref = _oracle_erased(o, c, chunks, er)
+            for e in er:
+                if e < c.k:
+                    assert np.array_equal(got[e], ref[e]), (cfg, sc, er, e)
+    finally:
+        clay_amd.set_exec_mode(prev)
