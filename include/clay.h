@@ -263,7 +263,9 @@ size_t clay_workspace_bytes(int device);
 /* Encode path selection (process-wide; tests and benchmarks).  Low byte = path:
  *   0 auto      -- the streaming kernel for q = 4, t = 4 codes with k = 9 / 10 (the
  *                  BASELINE (10,4,13)) and for (9,3,11) (k_stream_encode3: any sub-chunk
- *                  size >= 16 and any alignment); else the bit-sliced v1 kernel if the code has a
+ *                  size >= 16 and any alignment); (4,2,5): the line-local bit-sliced kernel
+ *                  (k_bs_encode1, "bitsliced-line-k4m2-w2048", any sub-chunk and alignment);
+ *                  else the bit-sliced v1 kernel if the code has a
  *                  compiled instantiation; else the byte-sliced fused kernel when the
  *                  parity is one y-section; else the staged plan executor.  Batches of
  *                  >= 4 stripes of <= 4 MiB of data run as one staged launch per level.
@@ -273,7 +275,7 @@ size_t clay_workspace_bytes(int device);
  *   1 staged    -- the plan executor (k_gexec), any code
  *   2 fused     -- byte-sliced fused kernel (q == m <= 4)
  *   3 bitsliced -- bit-sliced v1 (register loads); variant = lanes per column group
- *                  for (10,4,13): 0 (2), 1, 4
+ *                  for (10,4,13): 0 (2), 1, 4; (4,2,5) runs v1 here, not the line kernel
  *   5 stream    -- the streaming kernel (stream_encode.hpp); variant = loader waves
  *                  for (10,4,13): 0 (= 4, the default), 1, 2, 4; (9,4,12) always runs
  *                  4 loader waves (its variant is accepted and ignored); (9,3,11): 7 loader
@@ -294,9 +296,13 @@ int clay_set_encode_path(int mode);
  *                a single-launch local decode: one erasure in its section plus at most one
  *                more, or two in one section ({0}, {12}, {0,4}, {0,1}), on 256-byte row runs
  *                (k_stream_local256, last path "stream-local256", any sub-chunk), the others
- *                on 64-byte tiles (k_stream_local, "stream-local", sc % 8 == 0); 3 or 4
- *                erasures in distinct y-sections (sc % 8 == 0; the BASELINE
- *                {0,4,8,12} included) the fused decode v2 (k_stream_fused2, "stream-fused2")
+ *                on 64-byte tiles (k_stream_local, "stream-local", sc % 8 == 0) -- except
+ *                three erasures as two in one section and one in another ({0,1,4}), which
+ *                take the fused decode v2 first; 3 or 4 erasures with at most two per
+ *                y-section (sc % 8 == 0; the BASELINE {0,4,8,12} and the (2,1,1) / (2,2)
+ *                patterns included) the fused decode v2 (k_stream_fused2, "stream-fused2");
+ *                (4,2,5) with one erasure and every other chunk present: the single-erasure
+ *                bit-sliced decode (k_bs_decode1, "bs-decode1", any sub-chunk and alignment)
  *   1 grouped -- always the grouped executor (k_gexec, one launch per level)
  *   2 tile    -- the tile executor wherever its U slots fit, whatever the plan size
  *   (auto and stream: repair of (9,3,11), (10,4,13), (4,2,5) from all n - 1 other nodes runs
@@ -304,13 +310,15 @@ int clay_set_encode_path(int mode);
  *    CU; auto when the sub-chunk gives every CU a tile, stream for any sub-chunk >= 16 bytes
  *    of (9,3,11) / (10,4,13); last path "bs-repair-stream"), else k_bs_repair ("bs-repair"))
  *   3 stream  -- every decode a streaming kernel takes on it: the local decode where it takes
- *                the pattern, else the fused decode v2 (2-4 erasures in distinct sections);
- *                everything else as auto
+ *                the pattern (the (2,1) patterns: the fused decode v2 first), else the fused
+ *                decode v2 (2-4 erasures, at most two per section); everything else as auto
  *   5 stream-local -- every decode a local kernel takes on it ("stream-local256" /
  *                "stream-local"); else as auto
- *   6 stream-fused2 -- decodes of 2-4 erasures in distinct y-sections on the fused decode v2
- *                (k_stream_fused2, "stream-fused2"; ring of 10 - e node buffers: any two
- *                neighbouring sections hold <= 10 - e surviving real nodes); else as auto
+ *   6 stream-fused2 -- decodes of 2-4 erasures with at most two per y-section on the fused
+ *                decode v2 (k_stream_fused2, "stream-fused2"; ring of 10 - e node buffers: a
+ *                section's surviving real nodes fit it, two neighbouring sections that do not
+ *                run as a split step; the loader waves' round items fit their registers);
+ *                else as auto
  * (4 and 7 are retired: the single-launch decode of round 3 and the process-wide "codeword"
  * mode, now the per-call clay_decode_device_codeword.)
  * No CLAY_* environment variable is read on a call path; the measurement knobs (planner and
@@ -321,8 +329,8 @@ int clay_set_exec_mode(int mode);
 /* Plan executor the calling thread's last decode / repair / staged encode ran on:
  * "tile" (k_texec), "grouped" (k_gexec), "stream-local256" (k_stream_local256), "stream-local"
  * (k_stream_local), "stream-fused2"
- * (k_stream_fused2), "bs-repair-stream" (k_bs_repair_stream), "bs-repair" (k_bs_repair) or
- * "none". */
+ * (k_stream_fused2), "bs-decode1" (k_bs_decode1), "bs-repair-stream" (k_bs_repair_stream),
+ * "bs-repair" (k_bs_repair) or "none". */
 const char *clay_last_exec_path(void);
 
 /* Name of the path the last encode on this thread used ("fused-q4w128p8", "staged", ...). */
