@@ -93,9 +93,13 @@ struct StreamDec {
     // byte offset of row (c, g) within a node buffer
     __device__ static uint32_t row(uint32_t c, uint32_t g) { return c * 256u + ((g ^ (c & 3u)) << 6); }
 
-    // 8 dwords = the lane's 4 slots x 8 positions of one node at column cc
+    // 8 dwords = the lane's 4 slots x 8 positions of one node at column cc.  SWZ (k_stream_fused2's
+    // lane map, digit 2 of the column wave-uniform): the row swizzle comes from digit 1 instead,
+    // row (c, g) at c * 256 + (g ^ ((c >> 2) & 3)) * 64 -- the digit that varies across the lanes of
+    // a 32-lane ds_read_b64 group there, so own and companion reads stay conflict free
+    template <bool SWZ = false>
     __device__ static void read4(const uint8_t *buf, uint32_t cc, uint32_t poff, uint32_t (&d)[8]) {
-        const uint32_t b = cc * 256u + poff, cl = cc & 3u;
+        const uint32_t b = cc * 256u + poff, cl = SWZ ? ((cc >> 2) & 3u) : (cc & 3u);
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint2 v = *reinterpret_cast<const uint2 *>(buf + (b + ((uint32_t(g) ^ cl) << 6)));
@@ -155,13 +159,15 @@ struct StreamDec {
         uint32_t off[BPL];  // layer(c, g) * sc + 16 * piece, per block
         uint32_t pc16;      // 16 * piece
     };
+    template <bool SWZ = false>
     __device__ static void loader_init(Loader &L, uint32_t sc, int li, int lane) {
         const uint32_t k = uint32_t(lane);
         L.pc16 = (k & 3u) * 16u;
 #pragma unroll
         for (int j = 0; j < BPL; j++) {
             const uint32_t cc = uint32_t(li * BPL + j) * 4u + (k >> 4);
-            const uint32_t g = ((k >> 2) & 3u) ^ (k >> 4);
+            // the layer whose row lands in 64-byte slot (k >> 2) & 3 of column cc (read4's swizzle)
+            const uint32_t g = ((k >> 2) & 3u) ^ (SWZ ? ((cc >> 2) & 3u) : (k >> 4));
             L.off[j] = (layer0(cc) + g * wt(G)) * sc + L.pc16;
         }
     }
@@ -207,7 +213,8 @@ struct StreamDec {
     // straight-line PRT + fold code without the per-node branches, which the scheduler interleaves
     // across nodes; -1 (an ignored node in the section: fewer than 4 erasures) takes the run-time
     // copy.  PROBE 128 (probe library): always the run-time copy.
-    template <int PROBE, bool RT = false, bool SB = true, bool MULTI = false>
+    // SWZ (k_stream_fused2): read4's digit-1 swizzle, and the light section-2 step below
+    template <int PROBE, bool RT = false, bool SB = true, bool MULTI = false, bool SWZ = false>
     __device__ __forceinline__ static void phase_a(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0, int xeG,
                                    uint32_t (&S)[32], uint32_t R, uint64_t *tbar = nullptr) {
         sfor<4>([&](auto yc) BS_INL {
@@ -226,15 +233,15 @@ struct StreamDec {
             if constexpr ((PROBE & 2) != 0) return;
             if constexpr (!RT && (PROBE & 128) == 0) {
                 switch (a.scase[Y]) {
-                case 0: section<Y, 0, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 1: section<Y, 1, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 2: section<Y, 2, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 3: section<Y, 3, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                case 4: section<Y, 4, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
-                default: section<Y, -1, false, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 0: section<Y, 0, false, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 1: section<Y, 1, false, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 2: section<Y, 2, false, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 3: section<Y, 3, false, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                case 4: section<Y, 4, false, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R); break;
+                default: section<Y, -1, false, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R); break;
                 }
             } else {
-                section<Y, -1, RT, SB, MULTI>(a, smem, qbase, c0, poff0, xeG, S, R);
+                section<Y, -1, RT, SB, MULTI, SWZ>(a, smem, qbase, c0, poff0, xeG, S, R);
             }
         });
     }
@@ -250,7 +257,7 @@ struct StreamDec {
     // one step of phase A.  XE >= 0: the compile-time structure of scase XE (node (Y, XE) erased,
     // XE = 4: none; every other node used); XE = -1: the pattern's masks at run time
     // MULTI (k_stream_fused2<.., TWO>): the run-time copy also takes two erasures in section G
-    template <int Y, int XE, bool RT, bool SB, bool MULTI = false>
+    template <int Y, int XE, bool RT, bool SB, bool MULTI = false, bool SWZ = false>
     __device__ __forceinline__ static void section(const DecArgs &a, uint8_t *smem, uint32_t qbase, uint32_t c0, uint32_t poff0,
                                    int xeG, uint32_t (&S)[32], uint32_t R) {
         constexpr bool CT = XE >= 0;
@@ -271,6 +278,31 @@ struct StreamDec {
         if constexpr (Y != G) {
             const uint32_t sh = RT ? a.csh[Y] : uint32_t(csh(Y));
             const uint32_t cy = (c >> sh) & 3u;
+            if constexpr (SWZ && Y == 2 && csh(2) == 0) {
+                // k_stream_fused2's lane map makes digit 2 wave-uniform: where node (2, cy) is a
+                // shortened one (zero data), every PRT companion of the step is zero -- U = C for
+                // the alive used nodes, U = 0 for the shortened ones and Out = 0 for an erased one
+                // (no term): plain folds, no companion reads.  These light steps fall to waves 4-7,
+                // the younger wave of each SIMD (it loses the VALU arbitration; round-6 timing:
+                // 47 % slower on the same work)
+                const uint32_t cyu = __builtin_amdgcn_readfirstlane(cy);
+                if (4u * uint32_t(Y) + cyu >= uint32_t(KD) && 4u * uint32_t(Y) + cyu < uint32_t(S::K)) {
+                    sfor<4>([&](auto xc) BS_INL {
+                        constexpr int X = decltype(xc)::value;
+                        constexpr int I = 4 * Y + X;
+                        const bool alive_i = (aliveY >> X) & 1u;
+                        const bool used_i = CT ? X != XE : ((used_all >> I) & 1u);
+                        if (!(alive_i && used_i)) return;
+                        uint32_t u[8];
+                        read4<SWZ>(buf_of(X), c, poff, u);
+                        transpose8(u);
+                        fold<I, false>(u, S);
+                        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+                    });
+                    asm volatile("; phase A light copy %0" ::"i"(XE + 1));
+                    return;
+                }
+            }
             const bool comp_alive = (aliveY >> cy) & 1u;
             const uint8_t *cbuf = comp_alive ? buf_of(cy) : smem;
             sfor<4>([&](auto xc) BS_INL {
@@ -282,13 +314,13 @@ struct StreamDec {
                 if (!(used_i || erased_i)) return;
                 uint32_t o[8], cv[8], u[8];
                 if (alive_i) {
-                    read4(buf_of(X), c, poff, o);
+                    read4<SWZ>(buf_of(X), c, poff, o);
                 } else {
 #pragma unroll
                     for (int w = 0; w < 8; w++) o[w] = 0;
                 }
                 const uint32_t cc = (c & ~(3u << sh)) | (uint32_t(X) << sh);
-                read4(cbuf, cc, poff, cv);
+                read4<SWZ>(cbuf, cc, poff, cv);
                 const uint32_t keep = (comp_alive && cy != uint32_t(X)) ? 0xffffffffu : 0u;
                 const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
                 if (erased_i) {  // S += H_e Out(e, z): Out = gamma * companion (0 where red)
@@ -312,7 +344,7 @@ struct StreamDec {
             sfor<4>([&](auto xc) BS_INL {
                 constexpr int X = decltype(xc)::value;
                 if ((aliveY >> X) & 1u) {
-                    read4(buf_of(X), c, poff, o[X]);
+                    read4<SWZ>(buf_of(X), c, poff, o[X]);
                 } else {
 #pragma unroll
                     for (int w = 0; w < 8; w++) o[X][w] = 0;

@@ -80,7 +80,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         __builtin_amdgcn_s_setprio(3);
         const int li = wave - Kn::CWAVES;
         typename Kn::Loader L;
-        Kn::loader_init(L, sc, li, lane);
+        Kn::template loader_init<true>(L, sc, li, lane);
         const uint32_t lds0 = lds_addr_of(smem);
         const uint32_t nloads = ntile * NT;
         uint32_t issued = 0;
@@ -443,7 +443,15 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
     }
 
     // ---------------- compute waves ----------------
-    const uint32_t c0 = uint32_t(threadIdx.x) >> 3, p = uint32_t(threadIdx.x) & 7u;
+    // lane map (round 6): part p = lane & 7; column c = d0 d1 d2 with digit 2 from the wave (waves
+    // 4-7: d2 in {2, 3}, whose section-2 companions are the shortened nodes -- the light steps of
+    // StreamDec::section), digit 1 from lane bits 3-4 (the 32-lane ds_read_b64 groups see four
+    // digit-1 values: read4's SWZ row swizzle keeps own and companion reads conflict free), digit 0
+    // from wave bit 1 and lane bit 5
+    const uint32_t cw = uint32_t(wave), ck = (uint32_t(threadIdx.x) >> 3) & 7u;
+    const uint32_t c0 = ((((cw >> 1) & 1u) | (((ck >> 2) & 1u) << 1)) << 4) | ((ck & 3u) << 2) |
+                        ((cw & 1u) | (((cw >> 2) & 1u) << 1));
+    const uint32_t p = uint32_t(threadIdx.x) & 7u;
     const uint32_t emG = a.emask[G];
     const int xeG = emG ? __builtin_ctz(emG) : -1;
     constexpr bool TM = (PROBE & 16) != 0;
@@ -459,7 +467,7 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
             const uint32_t poff0 = 8u * p + ((straddle && p == 2u * pcs) ? 8u : 0u);
 #pragma unroll
             for (int w = 0; w < 32; w++) S[w] = 0;
-            Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false, TWO>(a, smem, k * NT, c0, poff0, xeG, S,
+            Kn::template phase_a<((PROBE & 4) ? 2 : 0) | (PROBE & 128), false, false, TWO, true>(a, smem, k * NT, c0, poff0, xeG, S,
                                                                                     RB, TM ? &tm_pabar : nullptr);
             // bit planes -> bytes
 #pragma unroll
@@ -573,10 +581,10 @@ __global__ __launch_bounds__((StreamDec<KD, G>::BLOCK)) void k_stream_fused2(Dec
         if constexpr (TM) tm_st += __builtin_amdgcn_s_memtime() - t0;
     }
     if constexpr (TM) {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            printf("f2-timing compute tiles %u total %lu phaseA %lu (barriers %lu) B_r %lu presolve %lu Cread+Swrite %lu - %lu "
+        if (blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == 256))  // compute waves 0 and 4 (one SIMD)
+            printf("f2-timing compute w%u tiles %u total %lu phaseA %lu (barriers %lu) B_r %lu presolve %lu Cread+Swrite %lu - %lu "
                    "stores %lu\n",
-                   ntile, (unsigned long)(__builtin_amdgcn_s_memtime() - tm_start), (unsigned long)tm_pa,
+                   unsigned(threadIdx.x >> 6), ntile, (unsigned long)(__builtin_amdgcn_s_memtime() - tm_start), (unsigned long)tm_pa,
                    (unsigned long)tm_pabar, (unsigned long)tm_br, (unsigned long)tm_pre, (unsigned long)tm_rd,
                    (unsigned long)tm_bw, (unsigned long)tm_st);
     }
