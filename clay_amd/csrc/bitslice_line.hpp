@@ -246,7 +246,7 @@ struct Enc1Kernel {
     }
 
     template <bool FULL, bool BT>
-    __device__ static void tile(const Enc1Args &a, uint64_t b0) {
+    __device__ static void tile(const Enc1Args &a, uint64_t b0, int64_t doff, int64_t poff) {
         for (int u = threadIdx.x; u < UNITS; u += BLOCK) {
             const int pg = u % PG, line = u / PG;
             const uint32_t z0 = uint32_t(line * Q);
@@ -266,14 +266,14 @@ struct Enc1Kernel {
                     constexpr int i = decltype(ic)::value;
                     constexpr int yi = i / Q, xi = i % Q;
                     uint32_t o[8], cv[8], t[8];
-                    ld32<FULL, BT>(o, a.data[i] + uint64_t(z) * a.sc + pos, nv);
+                    ld32<FULL, BT>(o, a.data[i] + doff + uint64_t(z) * a.sc + pos, nv);
                     // companion (yi, d) at z[yi := xi], d = z's digit yi (the line's)
                     const int d = int(z / uint32_t(wt(yi))) % Q;
                     const uint8_t *cn = a.data[yi * Q];
 #pragma unroll
                     for (int xx = 1; xx < Q; xx++) cn = d == xx ? a.data[yi * Q + xx] : cn;
                     const uint32_t zc = uint32_t(int(z) + (xi - d) * wt(yi));
-                    ld32<FULL, BT>(cv, cn + uint64_t(zc) * a.sc + pos, nv);
+                    ld32<FULL, BT>(cv, cn + doff + uint64_t(zc) * a.sc + pos, nv);
                     const uint32_t keep = d != xi ? 0xffffffffu : 0u;
                     const uint32_t ks = keep & 0xfefefefeu, kr = keep & 0x1d1d1d1du;
 #pragma unroll
@@ -307,7 +307,7 @@ struct Enc1Kernel {
                         });
                     }
                     transpose8(c);
-                    st32<FULL, BT>(a.par[x] + uint64_t(z0 + uint32_t(j)) * a.sc + pos, c, nv);
+                    st32<FULL, BT>(a.par[x] + poff + uint64_t(z0 + uint32_t(j)) * a.sc + pos, c, nv);
                 });
             });
         }
@@ -318,12 +318,16 @@ template <int KD, int M, int PG, bool BT = false>
 __global__ __launch_bounds__((Enc1Kernel<KD, M, PG>::BLOCK)) void k_bs_encode1(Enc1Args a) {
     using Kn = Enc1Kernel<KD, M, PG>;
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    const uint32_t ns = a.nstripes ? a.nstripes : 1u, total = a.ntiles * ns;
     for (uint32_t tix = slot; tix < a.tiles_per_xcd; tix += a.nslots) {
-        const uint32_t tile = xcd * a.tiles_per_xcd + tix;
-        if (tile >= a.ntiles) break;
+        // flattened (stripe, tile): each XCD streams a contiguous run of the stripes' tiles
+        const uint32_t ft = xcd * a.tiles_per_xcd + tix;
+        if (ft >= total) break;
+        const uint32_t stripe = ft / a.ntiles, tile = ft - stripe * a.ntiles;
         const uint64_t b0 = uint64_t(tile) * Kn::W;
-        if (b0 + Kn::W <= a.sc) Kn::template tile<true, BT>(a, b0);
-        else Kn::template tile<false, BT>(a, b0);
+        const int64_t doff = int64_t(stripe) * a.sdata, poff = int64_t(stripe) * a.spar;
+        if (b0 + Kn::W <= a.sc) Kn::template tile<true, BT>(a, b0, doff, poff);
+        else Kn::template tile<false, BT>(a, b0, doff, poff);
     }
 }
 

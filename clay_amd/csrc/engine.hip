@@ -1683,6 +1683,29 @@ static Error launch_bs_batch(CodeState &cs, int dev, const uint8_t *const *data0
     const uint64_t ntiles = (sc + Kn::W - 1) / Kn::W;
     // sub-chunks well under a tile would leave most lanes idle: the staged batch packs them
     if (sc < uint64_t(Kn::W) / 2 || ntiles * ns >= 0xFFFFFFFFull) return Error{};
+    if constexpr (KD == 4 && M == 2) {
+        // (4,2,5): the line-local kernel (bitslice_line.hpp), same 2048-position tiles
+        bs::Enc1Args e{};
+        for (int i = 0; i < KD; i++) e.data[i] = data0[i];
+        for (int x = 0; x < M; x++) e.par[x] = par0[x];
+        e.sc = sc;
+        e.ntiles = uint32_t(ntiles);
+        e.nstripes = uint32_t(ns);
+        e.sdata = sdata;
+        e.spar = spar;
+        e.tiles_per_xcd = uint32_t((ntiles * ns + 7) / 8);
+        e.nslots = std::min(e.tiles_per_xcd, uint32_t(std::max(1, dev_props(dev).cus / 8) * 8));
+        bool bt1 = sc % 8 != 0 || (sdata & 7) != 0 || (spar & 7) != 0;
+        for (int i = 0; i < KD; i++) bt1 |= (reinterpret_cast<uintptr_t>(e.data[i]) & 7u) != 0;
+        for (int x = 0; x < M; x++) bt1 |= (reinterpret_cast<uintptr_t>(e.par[x]) & 7u) != 0;
+        CLAY_HIP(launch_bs_encode1_kernel(KD, M, bt1, e, stream));
+        t_last_launches++;
+        char buf1[64];
+        std::snprintf(buf1, sizeof(buf1), "bitsliced-batch-line-k%dm%d-w%d", KD, M, Kn::W);
+        t_last_path = buf1;
+        *done = true;
+        return Error{};
+    }
     const int per_cu = std::max(1, int((160 * 1024) / (Kn::LDS_WORDS * 4)));
     bs::BsArgs a{};
     for (int i = 0; i < S::K; i++) a.data[i] = i < KD ? data0[i] : nullptr;

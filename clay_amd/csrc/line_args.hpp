@@ -20,6 +20,10 @@ struct Enc1Args {
     uint8_t *par[4];         // parity nodes (the last y-section)
     uint64_t sc;             // sub-chunk bytes
     uint32_t ntiles, tiles_per_xcd, nslots;
+    // batches: stripe s's nodes at data[i] + s * sdata, par[x] + s * spar (ntiles tiles per
+    // stripe, tiles_per_xcd over all nstripes * ntiles); nstripes = 0: one stripe
+    uint32_t nstripes;
+    int64_t sdata, spar;
 };
 
 }  // namespace bs

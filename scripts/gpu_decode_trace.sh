@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=${1:-dtr}
 mkdir -p "$R/gpurun_out/$TAG"
 export TMPDIR=/tmp
-for er in 0,4,8,12 0 0,4; do
+for er in ${ERS:-0,4,8,12 0 0,4}; do
   n=$(echo $er | tr , _)
   ( cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/$TAG/e$n" -o t -- python3 "$R/scripts/prof_decode.py" --er $er --iters 300 --prewarm-ms 250 ) > "$R/gpurun_out/$TAG/e$n.log" 2>&1 || { echo "trace $er failed"; tail -5 "$R/gpurun_out/$TAG/e$n.log"; exit 1; }
   w=$(grep -o "prewarm_calls [0-9]*" "$R/gpurun_out/$TAG/e$n.log" | awk '{print $2}')
